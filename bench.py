@@ -1,0 +1,245 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident RS(k,m) block erasure coding on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): RS(10,4) encode of 4096 x 1 MiB
+synthetic blocks per GPU, inputs resident in HBM before the timed region.
+A "step" = one encode pass over the whole batch (one kernel launch).  With
+--gpus N (torchrun, one process per GPU) every rank encodes its own 4096
+blocks (block-index partition, BASELINE.json C4 at N=8): weak scaling, no
+collective on the data path -- only the timing barrier / max-over-ranks.
+
+Printed JSON line (rank 0): the contract fields plus
+  roofline     : dominant kernel (gf_mac_kernel) algorithmic HBM bytes per
+                 launch, (k+m)*S*n, / its average HIP-event duration, vs 8 TB/s
+  cpu_baseline : the C oracle (scalar, table-driven) on this host's cores,
+                 same workload bytes, bounded sample (rank 0, N=1 only)
+  rebuild      : BASELINE.json C3 (RS(10,4), 4 random erasures per block)
+  end_to_end   : pinned host -> HBM -> host rate (PCIe-inclusive; not `value`)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+SEED = 0x6D656D6F
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md)
+METRIC = "GiB/s RS(k,m) encode+rebuild, device-resident batched blocks; % HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--k", type=int, default=10)
+    ap.add_argument("--m", type=int, default=4)
+    ap.add_argument("--block-bytes", type=int, default=1 << 20)
+    ap.add_argument("--blocks", type=int, default=4096, help="blocks per GPU")
+    ap.add_argument("--erasures", type=int, default=4)
+    ap.add_argument("--no-rebuild", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--sweep", action="store_true", help="also run the C5 mixed sweep")
+    return ap.parse_args()
+
+
+def timed_launches(torch, fn, steps, warmup, dist, stream):
+    """Warmup, then exactly `steps` launches bracketed by barrier+sync; per-
+    launch HIP events on `stream` (the stream the kernels are enqueued on)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kms = [a.elapsed_time(b) for a, b in ev]
+    return wall, kms
+
+
+def max_over_ranks(torch, dist, x):
+    if dist is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
+    """Time the C oracle (scalar 256x256-table codec) on this host, on a
+    bounded sample of the same workload; cross-check it against the GPU
+    parity of the same blocks.  Test infrastructure, never the product."""
+    from oracle import oracle as O
+    O.build()
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))  # the GPU box's CPU share is 16 per GPU
+    nb = 64
+    data = O.fill_blocks(SEED, 0, nb, B, k, S)
+    par = O.encode(k, m, S, data, threads=threads)
+    ok = bool(np.array_equal(par[:gpu_parity_sample.shape[0]], gpu_parity_sample))
+    # single core, a few blocks
+    t = time.perf_counter()
+    O.encode(k, m, S, data[:4], threads=1)
+    one = 4 * B / (time.perf_counter() - t) / 2**30
+    # all threads: repeat passes for ~`seconds`
+    passes, t = 0, time.perf_counter()
+    while True:
+        O.encode(k, m, S, data, threads=threads)
+        passes += 1
+        el = time.perf_counter() - t
+        if el >= seconds:
+            break
+    v = passes * nb * B / el / 2**30
+    return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": "RS(%d,%d) encode, %d x %d-byte blocks x %d passes (%.1f s), scalar C oracle; "
+                      "1-core %.3f GiB/s; bit-exact vs GPU on %d blocks: %s"
+                      % (k, m, nb, B, passes, el, one, gpu_parity_sample.shape[0], ok),
+            "single_core": round(one, 3), "bit_exact_vs_gpu": ok}
+
+
+def main():
+    args = parse()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist_mod
+        torch.cuda.set_device(local)
+        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        dist = dist_mod
+    else:
+        torch.cuda.set_device(0)
+    from memo_amd import ec
+
+    k, m, B, n, e = args.k, args.m, args.block_bytes, args.blocks, args.erasures
+    S = ec.shard_size(B, k)
+    stream = torch.cuda.current_stream()
+    codec = ec.Codec(local if world > 1 else 0)
+    codec.set_stream(stream)
+
+    data = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+    par = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+    codec.fill_blocks(SEED, rank * n, n, B, k, S, data)
+    torch.cuda.synchronize()
+
+    enc = lambda: codec.encode(k, m, data, par)  # noqa: E731
+    wall, kms = timed_launches(torch, enc, args.steps, args.warmup, dist, stream)
+    codec.synchronize()
+    wall = max_over_ranks(torch, dist, wall)
+    kavg_ms = float(np.mean(kms))
+    kavg_ms_max = max_over_ranks(torch, dist, kavg_ms)
+    payload = world * n * B * args.steps
+    value = payload / wall / 2**30
+    alg_bytes = (k + m) * S * n
+    achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "RS(%d,%d) encode, %d x %d-byte blocks per GPU (BASELINE.json %s)"
+                               % (k, m, n, B, "C2" if world == 1 else "C4"),
+                   "k": k, "m": m, "block_bytes": B, "blocks_per_gpu": n, "shard_bytes": S,
+                   "global_blocks": n * world, "parallelism": "block-index partition x%d" % world},
+        "roofline": {"bound": "hbm", "kernel": "gf_mac_kernel", "achieved": round(achieved, 1),
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
+                     "traffic": None, "bytes_per_launch": alg_bytes,
+                     "kernel_ms_avg": round(kavg_ms, 4), "kernel_ms_min": round(min(kms), 4),
+                     "kernel_ms_max_over_ranks": round(kavg_ms_max, 4),
+                     "read_only_frac": round(k * S * n / (kavg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            t = json.load(open(pmc))
+            key = "encode_%d_%d_%d_%d" % (k, m, B, n)
+            if key in t:
+                result["roofline"]["traffic"] = t[key]["hbm_bytes_per_launch"]
+                result["roofline"]["traffic_source"] = t[key]["source"]
+        except Exception:
+            pass
+
+    if not args.no_rebuild and e > 0:
+        s_idx, l_idx = ec.erasures(SEED, rank * n, n, k, m, e)
+        sd = torch.from_numpy(s_idx).cuda()
+        ld = torch.from_numpy(l_idx).cuda()
+        surv = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, data, par, sd, surv)
+        out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, data, par, ld, want)
+        reb = lambda: codec.rebuild(k, m, sd, surv, ld, out)  # noqa: E731
+        rwall, rkms = timed_launches(torch, reb, max(1, args.steps // 2), 2, dist, stream)
+        codec.synchronize()
+        ok = bool(torch.equal(out, want))
+        rwall = max_over_ranks(torch, dist, rwall)
+        rsteps = max(1, args.steps // 2)
+        rk = float(np.mean(rkms))
+        rbytes = (k + e) * S * n
+        result["rebuild"] = {
+            "workload": "RS(%d,%d) rebuild, %d random erasures/block, %d x %d-byte blocks per GPU "
+                        "(BASELINE.json C3)" % (k, m, e, n, B),
+            "value": round(world * n * B * rsteps / rwall / 2**30, 3), "unit": "GiB/s",
+            "ms_per_step": round(rwall / rsteps * 1e3, 4),
+            "step_ms_events": round(rk, 4),
+            "achieved_GBs": round(rbytes / (rk * 1e-3) / 1e9, 1),
+            "frac": round(rbytes / (rk * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "note": "step = decode-rows (batched GF inversion) + gf_mac_kernel",
+            "round_trip_bit_exact": ok}
+        del surv, out, want
+
+    if not args.no_e2e and world == 1:
+        ne = min(n, 1024)
+        hd = torch.empty((ne, k * S), dtype=torch.uint8).pin_memory()
+        hp = torch.empty((ne, m * S), dtype=torch.uint8).pin_memory()
+        hd.copy_(data[:ne].cpu())
+        codec.set_stream(None)
+        codec.encode(k, m, hd, hp)
+        t = time.perf_counter()
+        reps = 3
+        for _ in range(reps):
+            codec.encode(k, m, hd, hp)
+        el = time.perf_counter() - t
+        ok = bool(torch.equal(hp[:4].cuda(), par[:4]))
+        result["end_to_end"] = {
+            "workload": "RS(%d,%d) encode, %d x %d-byte blocks from pinned host memory, parity back "
+                        "to pinned host (HtoD+kernel+DtoH, 2-stream pipeline)" % (k, m, ne, B),
+            "value": round(reps * ne * B / el / 2**30, 3), "unit": "GiB/s", "bit_exact": ok}
+        codec.set_stream(stream)
+
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sample = par[:4].cpu().numpy()
+        result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, sample)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    codec.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

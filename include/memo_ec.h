@@ -1,0 +1,152 @@
+/*
+ * memo_ec.h -- C ABI of the MI355X (gfx950) block erasure codec.
+ *
+ * Drop-in point in infinit/memo (reference, read-only):
+ *   The codec replaces the byte movement of the immutable-block redundancy
+ *   path, which in the reference is N-way replication:
+ *     store  : Paxos::_store immutable branch + Details::send_immutable_block
+ *              src/memo/model/doughnut/consensus/Paxos.cc:1713-1732, 1815-1817,
+ *              315-391 (same B bytes sent to `factor` owners)
+ *              -> memo_ec_encode_batch (k data + m parity shards, one per owner)
+ *     fetch  : Paxos::Details::_fetch immutable branch, Paxos.cc:486-519
+ *              (first replica that answers) -> any k shards +
+ *              memo_ec_rebuild_batch when a data shard is missing
+ *     repair : LocalPeer::_disappeared_evict / _rebalance, Paxos.cc:1012-1246
+ *              (copy a surviving replica) -> memo_ec_rebuild_batch of the lost
+ *              shards, batched over all under-sharded blocks
+ *   The plugin surface it sits behind is unchanged:
+ *     consensus::Configuration / Consensus virtuals
+ *     src/memo/model/doughnut/Consensus.hh:24-174 (see host/ in this repo for
+ *     the ErasureConsensus plugin built on this ABI), payload = the
+ *     elle::Buffer of Block::data() (src/memo/model/blocks/Block.hh:142,
+ *     elle/src/elle/Buffer.hh:34) handed over as plain pointer + size.
+ *
+ * Convention: GF(2^8), polynomial 0x11D, generator 2;
+ * systematic ISA-L "cauchy1" generator: rows 0..k-1 identity, row i >= k,
+ * column j = 1 / (i XOR j).  Shard size S = memo_ec_shard_size(B, k) =
+ * round_up(ceil(B / k), 64); a block is zero-padded to k*S bytes and data
+ * shard j is bytes [j*S, (j+1)*S) of the padded block.
+ *
+ * Memory layout of a batch (all pointers are caller-owned):
+ *   data   : n blocks x k shards x S bytes, contiguous (block b at b*k*S)
+ *   parity : n blocks x m shards x S bytes (parity i of block b at (b*m+i)*S)
+ *   rebuild: surv_idx n x k (shard indices in [0,k+m)), surv n x k x S
+ *            (the survivors' bytes, in surv_idx order), lost_idx n x e,
+ *            out n x e x S (the rebuilt shards, in lost_idx order).
+ *
+ * Threading (mirrors elle::reactor::background, elle/src/elle/reactor/
+ * scheduler.cc:562-602, which runs CPU work on <= 16 pool threads): a ctx is
+ * used by one thread at a time; distinct ctxs are independent, so each pool
+ * thread owns one.  The library owns only device scratch and streams.
+ *
+ * Errors are returned as negative codes (memo_ec_strerror); the C++ plugin
+ * maps them to elle::Error-style exceptions (host/erasure_consensus.hh).
+ */
+#ifndef MEMO_EC_H
+#define MEMO_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MEMO_EC_VERSION 1
+
+/* Limits of this implementation. */
+#define MEMO_EC_MAX_K 64
+#define MEMO_EC_MAX_M 16
+#define MEMO_EC_MAX_SEGMENTS 12
+
+typedef struct memo_ec_ctx memo_ec_ctx;
+
+/* Where the buffers of a call live. */
+enum memo_ec_where {
+    MEMO_EC_HOST = 0,        /* pageable host memory: synchronous call      */
+    MEMO_EC_HOST_PINNED = 1, /* page-locked host memory: synchronous call   */
+    MEMO_EC_DEVICE = 2       /* device memory of the ctx's GPU: the call is
+                                enqueued on the ctx stream and returns; use
+                                memo_ec_synchronize for completion/errors   */
+};
+
+enum memo_ec_status {
+    MEMO_EC_OK = 0,
+    MEMO_EC_EINVAL = -1,    /* bad argument (k, m, S, e, pointer, where)    */
+    MEMO_EC_ENOMEM = -2,    /* device or pinned allocation failed           */
+    MEMO_EC_EHIP = -3,      /* HIP runtime error                            */
+    MEMO_EC_ESINGULAR = -4, /* survivor set cannot rebuild (duplicate or
+                               out-of-range shard indices)                  */
+    MEMO_EC_ENODEV = -5,    /* no such GPU                                  */
+    MEMO_EC_ERANGE = -6     /* k or m beyond MEMO_EC_MAX_K / MEMO_EC_MAX_M  */
+};
+
+/* One (k, m, S) group of blocks for the fused mixed-geometry encode. */
+typedef struct memo_ec_segment {
+    int k, m;
+    size_t S, n;
+    const uint8_t *data; /* device: n x k x S */
+    uint8_t *parity;     /* device: n x m x S */
+} memo_ec_segment;
+
+/* Context on GPU `device` (its own HIP stream, device scratch). */
+int memo_ec_ctx_create(int device, memo_ec_ctx **out);
+int memo_ec_ctx_destroy(memo_ec_ctx *ctx);
+
+/* Enqueue MEMO_EC_DEVICE work on `hip_stream` (a hipStream_t; NULL restores
+ * the ctx's own stream).  Lets a caller time kernels with its own events. */
+int memo_ec_set_stream(memo_ec_ctx *ctx, void *hip_stream);
+void *memo_ec_get_stream(memo_ec_ctx *ctx);
+
+/* Wait for the ctx's enqueued work; returns the first deferred error
+ * (e.g. MEMO_EC_ESINGULAR from a device-resident rebuild) and clears it. */
+int memo_ec_synchronize(memo_ec_ctx *ctx);
+
+/* round_up(ceil(B / k), 64) */
+size_t memo_ec_shard_size(size_t block_bytes, int k);
+
+/* Generator matrix (k+m) x k, row-major, into `out` (host memory). */
+int memo_ec_generator(int k, int m, uint8_t *out);
+
+/* parity_i = XOR_j C[k+i][j] * data_j for every block of the batch. */
+int memo_ec_encode_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
+                         const uint8_t *data, uint8_t *parity, int where);
+
+/* Rebuild the e lost shards of each block from its k survivors.  A lost
+ * index may name a data or a parity shard.  e == 0 is a no-op. */
+int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
+                          const uint8_t *surv_idx, const uint8_t *surv,
+                          const uint8_t *lost_idx, int e, uint8_t *out,
+                          int where);
+
+/* Per-block decode rows (n x e x k bytes, device) -- the batched GF(2^8)
+ * inversion that memo_ec_rebuild_batch runs before its multiply-accumulate.
+ * Device pointers only; asynchronous on the ctx stream. */
+int memo_ec_decode_rows(memo_ec_ctx *ctx, int k, int m, size_t n,
+                        const uint8_t *surv_idx, const uint8_t *lost_idx,
+                        int e, uint8_t *rows);
+
+/* Fused encode of up to MEMO_EC_MAX_SEGMENTS device-resident segments with
+ * different (k, m, S) in one launch.  Asynchronous on the ctx stream. */
+int memo_ec_encode_segments(memo_ec_ctx *ctx, int nseg,
+                            const memo_ec_segment *segs);
+
+/* Synthetic workload helpers (device memory; asynchronous on the ctx
+ * stream).  Bytes and erasure patterns follow DESIGN.md section 6. */
+int memo_ec_fill_blocks(memo_ec_ctx *ctx, uint64_t seed, uint64_t first_block,
+                        size_t n, size_t B, int k, size_t S, uint8_t *out);
+int memo_ec_erasures(uint64_t seed, uint64_t first_block, size_t n, int k,
+                     int m, int e, uint8_t *surv_idx, uint8_t *lost_idx);
+/* out[b][r] = shard idx[b][r] of block b, shards drawn from data (index < k)
+ * or parity (index >= k).  Device memory; asynchronous. */
+int memo_ec_gather_shards(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
+                          const uint8_t *data, const uint8_t *parity,
+                          const uint8_t *idx, int cnt, uint8_t *out);
+
+const char *memo_ec_strerror(int code);
+int memo_ec_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MEMO_EC_H */

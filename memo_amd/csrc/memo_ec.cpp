@@ -1,0 +1,539 @@
+// memo_ec.cpp -- C ABI of the gfx950 erasure codec (include/memo_ec.h).
+//
+// Host side of the drop-in boundary: validates arguments, plans the
+// multiply-accumulate launch (ec_kernels.hip), runs device-resident calls
+// asynchronously on the ctx stream and host-memory calls through a
+// double-buffered HtoD -> kernel -> DtoH pipeline.  No CPU fallback exists:
+// every byte of parity/rebuild output is produced by the HIP kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/memo_ec.h"
+#include "ec_kernels.h"
+
+using namespace memo_ec;
+
+struct memo_ec_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;      // ctx stream
+  hipStream_t stream = nullptr;   // stream MEMO_EC_DEVICE work goes to
+  hipStream_t aux[2] = {nullptr, nullptr};  // host-pipeline streams
+  uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
+  uint8_t* d_rows = nullptr;      // decode rows scratch
+  size_t rows_cap = 0;
+  // host pipeline: device slots and pinned bounce buffers
+  uint8_t* d_slot[2] = {nullptr, nullptr};
+  size_t slot_cap = 0;
+  uint8_t* h_slot[2] = {nullptr, nullptr};
+  size_t hslot_cap = 0;
+  int deferred = 0;
+  int cus = 256;
+};
+
+namespace {
+
+constexpr size_t kLdsBudget = 48 * 1024;  // table LDS per workgroup (flat mapping)
+constexpr size_t kPipeBytes = 64ull << 20;  // host pipeline batch (input bytes)
+
+int hip_rc(hipError_t e) {
+  if (e == hipSuccess) return MEMO_EC_OK;
+  if (e == hipErrorOutOfMemory) return MEMO_EC_ENOMEM;
+  return MEMO_EC_EHIP;
+}
+#define HIPCHK(x)                       \
+  do {                                  \
+    hipError_t _e = (x);                \
+    if (_e != hipSuccess) return hip_rc(_e); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != d) (void)hipSetDevice(d);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+int check_km(int k, int m) {
+  if (k < 1 || m < 0) return MEMO_EC_EINVAL;
+  if (k > MEMO_EC_MAX_K || m > MEMO_EC_MAX_M) return MEMO_EC_ERANGE;
+  if (k + m > 256) return MEMO_EC_EINVAL;
+  return MEMO_EC_OK;
+}
+
+// One segment of a MAC launch plus the compile-time bounds it needs.
+struct Plan {
+  MacSeg seg{};
+  int KC = 4, R = 1;
+  size_t lds = 0;  // table bytes (without the 768-byte GF image)
+  bool shared = true;
+};
+
+Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* in,
+                  uint64_t in_bs, uint64_t in_ss, uint8_t* out, uint64_t out_bs, uint64_t out_ss,
+                  const uint8_t* coef, uint64_t coef_bs, int KC, int R) {
+  Plan p;
+  p.KC = KC;
+  p.R = R;
+  p.shared = coef_bs == 0;
+  MacSeg& s = p.seg;
+  s.in = in; s.out = out; s.coef = coef;
+  s.in_bstride = in_bs; s.in_sstride = in_ss;
+  s.out_bstride = out_bs; s.out_sstride = out_ss;
+  s.coef_bstride = coef_bs;
+  s.n = n; s.kin = kin; s.r = r;
+  s.chunks = (uint32_t)(S / 16);
+  const uint32_t kpad = (kin + KC - 1) / KC * KC;
+  const size_t set_bytes = (size_t)R * kpad * 32;
+  const uint64_t C = s.chunks;
+  if (p.shared) {
+    s.flat = 1;
+    p.lds = set_bytes;
+  } else {
+    const uint64_t nsets = (MAC_UNITS + C - 1) / C + 1;
+    if (nsets * set_bytes <= kLdsBudget) {
+      s.flat = 1;
+      p.lds = nsets * set_bytes;
+    } else {
+      s.flat = 0;
+      p.lds = set_bytes;
+    }
+  }
+  if (s.flat) {
+    s.tiles = (n * C + MAC_UNITS - 1) / MAC_UNITS;
+    s.tiles_per_block = 0;
+  } else {
+    s.tiles_per_block = (C + MAC_UNITS - 1) / MAC_UNITS;
+    s.tiles = n * s.tiles_per_block;
+  }
+  return p;
+}
+
+// Launch 1..MEMO_EC_MAX_SEGMENTS planned segments as one kernel.  All must
+// share `shared`; KC/R are unified to the common bound.
+int launch_plans(memo_ec_ctx* ctx, std::vector<Plan>& plans, hipStream_t st) {
+  if (plans.empty()) return MEMO_EC_OK;
+  MacLaunch L{};
+  L.nseg = 0;
+  uint64_t total_tiles = 0;
+  size_t lds = 0;
+  int KC = plans[0].KC, R = 0;
+  const bool shared = plans[0].shared;
+  for (auto& p : plans) {
+    if (p.KC != KC) return MEMO_EC_EINVAL;
+    if (p.shared != shared) return MEMO_EC_EINVAL;
+    R = std::max(R, p.R);
+    total_tiles += p.seg.tiles;
+  }
+  if (total_tiles == 0) return MEMO_EC_OK;
+  // Workgroup budget: enough waves to keep every CU streaming, each
+  // workgroup walking a contiguous range of tiles.
+  const uint64_t cap = (uint64_t)ctx->cus * 8;
+  const uint64_t want = std::min<uint64_t>(total_tiles, cap);
+  uint32_t wg = 0;
+  for (auto& p : plans) {
+    if (p.seg.tiles == 0) continue;
+    uint64_t w = (want * p.seg.tiles + total_tiles - 1) / total_tiles;
+    w = std::max<uint64_t>(1, std::min<uint64_t>(w, p.seg.tiles));
+    p.seg.wg_begin = wg;
+    p.seg.wgs = (uint32_t)w;
+    wg += (uint32_t)w;
+    // recompute LDS with the unified R
+    const uint32_t kpad = (p.seg.kin + KC - 1) / KC * KC;
+    const size_t set_bytes = (size_t)R * kpad * 32;
+    size_t need = set_bytes;
+    if (!shared && p.seg.flat) need = ((MAC_UNITS + p.seg.chunks - 1) / p.seg.chunks + 1) * set_bytes;
+    lds = std::max(lds, need);
+    L.seg[L.nseg++] = p.seg;
+  }
+  if (lds + 768 > 160 * 1024) return MEMO_EC_ERANGE;
+  hipError_t e = launch_mac(KC, R, shared, L, wg, 768 + lds, st);
+  return hip_rc(e);
+}
+
+int ensure_rows(memo_ec_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->rows_cap) return MEMO_EC_OK;
+  if (ctx->d_rows) {
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipFree(ctx->d_rows));
+    ctx->d_rows = nullptr;
+  }
+  size_t cap = std::max<size_t>(bytes, 1 << 20);
+  HIPCHK(hipMalloc(&ctx->d_rows, cap));
+  ctx->rows_cap = cap;
+  return MEMO_EC_OK;
+}
+
+int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
+  if (dev_bytes > ctx->slot_cap) {
+    for (auto& st : ctx->aux) HIPCHK(hipStreamSynchronize(st));
+    for (auto& p : ctx->d_slot) {
+      if (p) HIPCHK(hipFree(p));
+      p = nullptr;
+    }
+    for (auto& p : ctx->d_slot) HIPCHK(hipMalloc(&p, dev_bytes));
+    ctx->slot_cap = dev_bytes;
+  }
+  if (host_bytes > ctx->hslot_cap) {
+    for (auto& st : ctx->aux) HIPCHK(hipStreamSynchronize(st));
+    for (auto& p : ctx->h_slot) {
+      if (p) HIPCHK(hipHostFree(p));
+      p = nullptr;
+    }
+    for (auto& p : ctx->h_slot) HIPCHK(hipHostMalloc(&p, host_bytes, hipHostMallocDefault));
+    ctx->hslot_cap = host_bytes;
+  }
+  return MEMO_EC_OK;
+}
+
+// Device-resident encode on stream st.
+int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* data,
+                  uint8_t* parity, hipStream_t st) {
+  std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)m, S, n, data, (uint64_t)k * S, S,
+                                       parity, (uint64_t)m * S, S, nullptr, 0, mac_kchunk(k),
+                                       mac_rbound(m))};
+  return launch_plans(ctx, plans, st);
+}
+
+// Device-resident rebuild on stream st: decode rows then the MAC.
+int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
+                   const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
+                   uint8_t* rows, hipStream_t st) {
+  DecodeArgs a{surv_idx, lost_idx, rows, ctx->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e};
+  HIPCHK(launch_decode_rows(a, st));
+  std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, n, surv, (uint64_t)k * S, S,
+                                       out, (uint64_t)e * S, S, rows, (uint64_t)e * k,
+                                       mac_kchunk(k), mac_rbound(e))};
+  return launch_plans(ctx, plans, st);
+}
+
+int take_deferred(memo_ec_ctx* ctx) {
+  uint32_t st = 0;
+  HIPCHK(hipMemcpy(&st, ctx->d_status, sizeof st, hipMemcpyDeviceToHost));
+  if (st) {
+    const uint32_t z = 0;
+    HIPCHK(hipMemcpy(ctx->d_status, &z, sizeof z, hipMemcpyHostToDevice));
+  }
+  int rc = ctx->deferred;
+  ctx->deferred = 0;
+  if (rc == MEMO_EC_OK && (st & 1u)) rc = MEMO_EC_ESINGULAR;
+  return rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int memo_ec_version(void) { return MEMO_EC_VERSION; }
+
+const char* memo_ec_strerror(int code) {
+  switch (code) {
+    case MEMO_EC_OK: return "ok";
+    case MEMO_EC_EINVAL: return "invalid argument";
+    case MEMO_EC_ENOMEM: return "out of memory";
+    case MEMO_EC_EHIP: return "HIP runtime error";
+    case MEMO_EC_ESINGULAR: return "survivor shards cannot rebuild the block";
+    case MEMO_EC_ENODEV: return "no such GPU";
+    case MEMO_EC_ERANGE: return "k or m beyond this build's limits";
+    default: return "unknown error";
+  }
+}
+
+size_t memo_ec_shard_size(size_t B, int k) {
+  if (k < 1) return 0;
+  size_t per = (B + (size_t)k - 1) / (size_t)k;
+  if (per == 0) per = 1;
+  return (per + 63) & ~(size_t)63;
+}
+
+int memo_ec_generator(int k, int m, uint8_t* out) {
+  if (int rc = check_km(k, m)) return rc;
+  if (!out) return MEMO_EC_EINVAL;
+  const uint8_t* lg = host_gf_log();
+  const uint8_t* ex = host_gf_exp();
+  std::memset(out, 0, (size_t)(k + m) * k);
+  for (int i = 0; i < k; ++i) out[(size_t)i * k + i] = 1;
+  for (int i = k; i < k + m; ++i)
+    for (int j = 0; j < k; ++j) out[(size_t)i * k + j] = ex[255 - lg[i ^ j]];
+  return MEMO_EC_OK;
+}
+
+int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
+  if (!out) return MEMO_EC_EINVAL;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return MEMO_EC_ENODEV;
+  DeviceGuard g(device);
+  auto* c = new (std::nothrow) memo_ec_ctx;
+  if (!c) return MEMO_EC_ENOMEM;
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    c->cus = prop.multiProcessorCount;
+  int rc = MEMO_EC_OK;
+  if ((rc = hip_rc(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipMalloc(&c->d_status, 256))) ||
+      (rc = hip_rc(hipMemset(c->d_status, 0, 256)))) {
+    memo_ec_ctx_destroy(c);
+    return rc;
+  }
+  c->stream = c->own;
+  *out = c;
+  return MEMO_EC_OK;
+}
+
+int memo_ec_ctx_destroy(memo_ec_ctx* c) {
+  if (!c) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  if (c->own) (void)hipStreamSynchronize(c->own);
+  if (c->stream && c->stream != c->own) (void)hipStreamSynchronize(c->stream);
+  for (auto& st : c->aux)
+    if (st) (void)hipStreamSynchronize(st);
+  for (auto& p : c->d_slot)
+    if (p) (void)hipFree(p);
+  for (auto& p : c->h_slot)
+    if (p) (void)hipHostFree(p);
+  if (c->d_rows) (void)hipFree(c->d_rows);
+  if (c->d_status) (void)hipFree(c->d_status);
+  for (auto& st : c->aux)
+    if (st) (void)hipStreamDestroy(st);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return MEMO_EC_OK;
+}
+
+int memo_ec_set_stream(memo_ec_ctx* c, void* s) {
+  if (!c) return MEMO_EC_EINVAL;
+  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+  return MEMO_EC_OK;
+}
+
+void* memo_ec_get_stream(memo_ec_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
+
+int memo_ec_synchronize(memo_ec_ctx* c) {
+  if (!c) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return take_deferred(c);
+}
+
+int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const uint8_t* data,
+                         uint8_t* parity, int where) {
+  if (!c) return MEMO_EC_EINVAL;
+  if (int rc = check_km(k, m)) return rc;
+  if (m == 0 || n == 0) return MEMO_EC_OK;
+  if (S == 0 || S % 64 != 0 || !data || !parity) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  if (where == MEMO_EC_DEVICE) return encode_device(c, k, m, S, n, data, parity, c->stream);
+  if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
+
+  // Host pipeline: batches of nb blocks alternate between two slots/streams;
+  // batch i+1's copy-in overlaps batch i's kernel and copy-out.
+  const size_t in_b = (size_t)k * S, out_b = (size_t)m * S;
+  size_t nb = std::max<size_t>(1, kPipeBytes / in_b);
+  nb = std::min(nb, n);
+  const bool pinned = where == MEMO_EC_HOST_PINNED;
+  if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
+  const size_t nbatch = (n + nb - 1) / nb;
+  std::vector<size_t> pend_off(2, 0), pend_cnt(2, 0);
+  auto drain = [&](int s) -> int {
+    if (!pend_cnt[s]) return MEMO_EC_OK;
+    HIPCHK(hipStreamSynchronize(c->aux[s]));
+    if (!pinned)
+      std::memcpy(parity + pend_off[s] * out_b, c->h_slot[s] + pend_cnt[s] * in_b,
+                  pend_cnt[s] * out_b);
+    pend_cnt[s] = 0;
+    return MEMO_EC_OK;
+  };
+  for (size_t bi = 0; bi < nbatch; ++bi) {
+    const int s = (int)(bi & 1);
+    if (int rc = drain(s)) return rc;
+    const size_t b0 = bi * nb, cnt = std::min(nb, n - b0);
+    uint8_t* din = c->d_slot[s];
+    uint8_t* dout = din + cnt * in_b;
+    const uint8_t* src = data + b0 * in_b;
+    if (!pinned) {
+      std::memcpy(c->h_slot[s], src, cnt * in_b);
+      src = c->h_slot[s];
+    }
+    HIPCHK(hipMemcpyAsync(din, src, cnt * in_b, hipMemcpyHostToDevice, c->aux[s]));
+    if (int rc = encode_device(c, k, m, S, cnt, din, dout, c->aux[s])) return rc;
+    uint8_t* dst = pinned ? parity + b0 * out_b : c->h_slot[s] + cnt * in_b;
+    HIPCHK(hipMemcpyAsync(dst, dout, cnt * out_b, hipMemcpyDeviceToHost, c->aux[s]));
+    pend_off[s] = b0;
+    pend_cnt[s] = cnt;
+  }
+  for (int s = 0; s < 2; ++s)
+    if (int rc = drain(s)) return rc;
+  return MEMO_EC_OK;
+}
+
+int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* surv_idx,
+                        const uint8_t* lost_idx, int e, uint8_t* rows) {
+  if (!c) return MEMO_EC_EINVAL;
+  if (int rc = check_km(k, m)) return rc;
+  if (e < 0 || e > m) return MEMO_EC_EINVAL;
+  if (n == 0 || e == 0) return MEMO_EC_OK;
+  if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e};
+  return hip_rc(launch_decode_rows(a, c->stream));
+}
+
+int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
+                          const uint8_t* surv_idx, const uint8_t* surv, const uint8_t* lost_idx,
+                          int e, uint8_t* out, int where) {
+  if (!c) return MEMO_EC_EINVAL;
+  if (int rc = check_km(k, m)) return rc;
+  if (e < 0 || e > m) return MEMO_EC_EINVAL;
+  if (e == 0 || n == 0) return MEMO_EC_OK;
+  if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  if (where == MEMO_EC_DEVICE) {
+    if (int rc = ensure_rows(c, n * (size_t)e * k)) return rc;
+    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_rows, c->stream);
+  }
+  if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
+
+  const size_t in_b = (size_t)k * S, out_b = (size_t)e * S;
+  const size_t idx_b = (size_t)k + e;
+  size_t nb = std::max<size_t>(1, kPipeBytes / in_b);
+  nb = std::min(nb, n);
+  const bool pinned = where == MEMO_EC_HOST_PINNED;
+  // slot layout: [surv | out | surv_idx | lost_idx], host bounce likewise
+  const size_t slot = nb * (in_b + out_b + idx_b);
+  if (int rc = ensure_slots(c, slot, slot)) return rc;
+  if (int rc = ensure_rows(c, 2 * nb * (size_t)e * k)) return rc;
+  const size_t nbatch = (n + nb - 1) / nb;
+  std::vector<size_t> pend_off(2, 0), pend_cnt(2, 0);
+  auto drain = [&](int s) -> int {
+    if (!pend_cnt[s]) return MEMO_EC_OK;
+    HIPCHK(hipStreamSynchronize(c->aux[s]));
+    if (!pinned)
+      std::memcpy(out + pend_off[s] * out_b, c->h_slot[s] + pend_cnt[s] * in_b,
+                  pend_cnt[s] * out_b);
+    pend_cnt[s] = 0;
+    return MEMO_EC_OK;
+  };
+  for (size_t bi = 0; bi < nbatch; ++bi) {
+    const int s = (int)(bi & 1);
+    if (int rc = drain(s)) return rc;
+    const size_t b0 = bi * nb, cnt = std::min(nb, n - b0);
+    uint8_t* dsurv = c->d_slot[s];
+    uint8_t* dout = dsurv + cnt * in_b;
+    uint8_t* dsidx = dout + cnt * out_b;
+    uint8_t* dlidx = dsidx + cnt * k;
+    uint8_t* h = c->h_slot[s];
+    // indices always go through the pinned slot (small)
+    std::memcpy(h + cnt * (in_b + out_b), surv_idx + b0 * k, cnt * k);
+    std::memcpy(h + cnt * (in_b + out_b) + cnt * k, lost_idx + b0 * e, cnt * e);
+    HIPCHK(hipMemcpyAsync(dsidx, h + cnt * (in_b + out_b), cnt * idx_b, hipMemcpyHostToDevice,
+                          c->aux[s]));
+    const uint8_t* src = surv + b0 * in_b;
+    if (!pinned) {
+      std::memcpy(h, src, cnt * in_b);
+      src = h;
+    }
+    HIPCHK(hipMemcpyAsync(dsurv, src, cnt * in_b, hipMemcpyHostToDevice, c->aux[s]));
+    uint8_t* rows = c->d_rows + (size_t)s * nb * e * k;
+    if (int rc = rebuild_device(c, k, m, S, cnt, dsidx, dsurv, dlidx, e, dout, rows, c->aux[s]))
+      return rc;
+    uint8_t* dst = pinned ? out + b0 * out_b : h + cnt * in_b;
+    HIPCHK(hipMemcpyAsync(dst, dout, cnt * out_b, hipMemcpyDeviceToHost, c->aux[s]));
+    pend_off[s] = b0;
+    pend_cnt[s] = cnt;
+  }
+  for (int s = 0; s < 2; ++s)
+    if (int rc = drain(s)) return rc;
+  return take_deferred(c);
+}
+
+int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* segs) {
+  if (!c || nseg < 0 || nseg > MEMO_EC_MAX_SEGMENTS || (nseg && !segs)) return MEMO_EC_EINVAL;
+  // common chunk: the specialised k when all segments share it, else 4
+  int KC = -1;
+  for (int i = 0; i < nseg; ++i) {
+    if (int rc = check_km(segs[i].k, segs[i].m)) return rc;
+    if (segs[i].m == 0 || segs[i].n == 0) continue;
+    if (segs[i].S == 0 || segs[i].S % 64 || !segs[i].data || !segs[i].parity)
+      return MEMO_EC_EINVAL;
+    const int kc = mac_kchunk(segs[i].k);
+    KC = (KC < 0 || KC == kc) ? kc : 4;
+  }
+  if (KC < 0) return MEMO_EC_OK;
+  int R = 1;
+  for (int i = 0; i < nseg; ++i) R = std::max(R, mac_rbound(segs[i].m));
+  DeviceGuard g(c->device);
+  std::vector<Plan> plans;
+  for (int i = 0; i < nseg; ++i) {
+    const auto& s = segs[i];
+    if (s.m == 0 || s.n == 0) continue;
+    plans.push_back(plan_segment((uint32_t)s.k, (uint32_t)s.m, s.S, s.n, s.data,
+                                 (uint64_t)s.k * s.S, s.S, s.parity, (uint64_t)s.m * s.S, s.S,
+                                 nullptr, 0, KC, R));
+  }
+  return launch_plans(c, plans, c->stream);
+}
+
+int memo_ec_fill_blocks(memo_ec_ctx* c, uint64_t seed, uint64_t first_block, size_t n, size_t B,
+                        int k, size_t S, uint8_t* out) {
+  if (!c || k < 1 || S % 16 || (size_t)k * S < B || (n && !out)) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  FillArgs a{out, seed, first_block, n, B, (uint64_t)k * S};
+  return hip_rc(launch_fill(a, c->stream));
+}
+
+int memo_ec_gather_shards(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const uint8_t* data,
+                          const uint8_t* parity, const uint8_t* idx, int cnt, uint8_t* out) {
+  if (!c || check_km(k, m) || S % 16 || cnt < 0 || (n && cnt && (!data || !idx || !out)))
+    return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  GatherArgs a{data, parity, idx, out, S, n, (uint32_t)k, (uint32_t)m, (uint32_t)cnt};
+  return hip_rc(launch_gather(a, c->stream));
+}
+
+static inline uint64_t sm64_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+int memo_ec_erasures(uint64_t seed, uint64_t first_block, size_t n, int k, int m, int e,
+                     uint8_t* surv_idx, uint8_t* lost_idx) {
+  if (check_km(k, m) || e < 0 || e > m || (n && (!surv_idx || (e && !lost_idx))))
+    return MEMO_EC_EINVAL;
+  const int total = k + m;
+  const uint64_t gamma = 0x9E3779B97F4A7C15ull;
+  for (size_t b = 0; b < n; ++b) {
+    const uint64_t key = sm64_mix(sm64_mix(seed + 1) ^ ((first_block + b) * gamma));
+    uint8_t perm[256], lost[256] = {0};
+    for (int i = 0; i < total; ++i) perm[i] = (uint8_t)i;
+    for (int i = 0; i < e; ++i) {
+      const uint64_t w = sm64_mix(key + (uint64_t)(i + 1) * gamma);
+      const int r = i + (int)(w % (uint64_t)(total - i));
+      std::swap(perm[i], perm[r]);
+      lost[perm[i]] = 1;
+    }
+    int li = 0, si = 0;
+    for (int i = 0; i < total; ++i) {
+      if (lost[i]) lost_idx[b * e + li++] = (uint8_t)i;
+      else if (si < k) surv_idx[b * k + si++] = (uint8_t)i;
+    }
+  }
+  return MEMO_EC_OK;
+}
+
+}  // extern "C"

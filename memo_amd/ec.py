@@ -1,0 +1,246 @@
+"""Python binding of libmemo_ec.so (the C ABI in include/memo_ec.h).
+
+This is plumbing for tests and bench.py: every call goes through the C ABI
+into the gfx950 HIP kernels.  There is no CPU fallback -- if the library is
+missing or no GPU is present, the calls raise.
+
+Device buffers are torch uint8 CUDA tensors (PyTorch-ROCm provides the HBM
+allocations and streams); host buffers are numpy uint8 arrays.
+
+Reference call sites the codec replaces (infinit/memo, read-only):
+  encode  <- Paxos::Details::send_immutable_block, consensus/Paxos.cc:315-391
+  rebuild <- Paxos::Details::_fetch (immutable), Paxos.cc:486-519, and the
+             _rebalance repair loop, Paxos.cc:1012-1246
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libmemo_ec.so")
+
+HOST, HOST_PINNED, DEVICE = 0, 1, 2
+MAX_K, MAX_M, MAX_SEGMENTS = 64, 16, 12
+
+_u8p = ctypes.c_void_p
+_sz = ctypes.c_size_t
+
+
+class MemoECError(RuntimeError):
+    """Raised for a negative memo_ec status code (memo_ec_strerror text)."""
+
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = _lib().memo_ec_strerror(code).decode() if _LIB is not None else str(code)
+        super().__init__("%s%s (code %d)" % (what + ": " if what else "", msg, code))
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [("k", ctypes.c_int), ("m", ctypes.c_int), ("S", _sz), ("n", _sz),
+                ("data", ctypes.c_void_p), ("parity", ctypes.c_void_p)]
+
+
+_LIB = None
+
+EXPORTS = [
+    "memo_ec_ctx_create", "memo_ec_ctx_destroy", "memo_ec_set_stream", "memo_ec_get_stream",
+    "memo_ec_synchronize", "memo_ec_shard_size", "memo_ec_generator", "memo_ec_encode_batch",
+    "memo_ec_rebuild_batch", "memo_ec_decode_rows", "memo_ec_encode_segments",
+    "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards", "memo_ec_strerror",
+    "memo_ec_version",
+]
+
+
+def _lib():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libmemo_ec.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        c_int, c_u64 = ctypes.c_int, ctypes.c_uint64
+        L.memo_ec_ctx_create.argtypes = [c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.memo_ec_ctx_destroy.argtypes = [ctypes.c_void_p]
+        L.memo_ec_set_stream.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.memo_ec_get_stream.argtypes = [ctypes.c_void_p]
+        L.memo_ec_get_stream.restype = ctypes.c_void_p
+        L.memo_ec_synchronize.argtypes = [ctypes.c_void_p]
+        L.memo_ec_shard_size.argtypes = [_sz, c_int]
+        L.memo_ec_shard_size.restype = _sz
+        L.memo_ec_generator.argtypes = [c_int, c_int, _u8p]
+        L.memo_ec_encode_batch.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p, c_int]
+        L.memo_ec_rebuild_batch.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
+                                            _u8p, c_int, _u8p, c_int]
+        L.memo_ec_decode_rows.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _u8p, _u8p, c_int, _u8p]
+        L.memo_ec_encode_segments.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(Segment)]
+        L.memo_ec_fill_blocks.argtypes = [ctypes.c_void_p, c_u64, c_u64, _sz, _sz, c_int, _sz, _u8p]
+        L.memo_ec_erasures.argtypes = [c_u64, c_u64, _sz, c_int, c_int, c_int, _u8p, _u8p]
+        L.memo_ec_gather_shards.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
+                                            _u8p, c_int, _u8p]
+        L.memo_ec_strerror.argtypes = [c_int]
+        L.memo_ec_strerror.restype = ctypes.c_char_p
+        L.memo_ec_version.restype = c_int
+        _LIB = L
+    return _LIB
+
+
+def _check(rc, what=""):
+    if rc != 0:
+        raise MemoECError(rc, what)
+
+
+def shard_size(block_bytes, k):
+    """S = round_up(ceil(B / k), 64) -- the shard size of a B-byte block."""
+    return _lib().memo_ec_shard_size(block_bytes, k)
+
+
+def generator(k, m):
+    """(k+m) x k generator matrix (identity over ISA-L cauchy1 rows)."""
+    out = np.zeros((k + m, k), dtype=np.uint8)
+    _check(_lib().memo_ec_generator(k, m, out.ctypes.data), "generator")
+    return out
+
+
+def erasures(seed, first_block, n, k, m, e):
+    """Synthetic erasure patterns (host): (surv_idx n x k, lost_idx n x e)."""
+    s = np.zeros((n, k), dtype=np.uint8)
+    l = np.zeros((n, max(e, 1)), dtype=np.uint8)
+    _check(_lib().memo_ec_erasures(seed, first_block, n, k, m, e, s.ctypes.data, l.ctypes.data),
+           "erasures")
+    return s, l[:, :e].copy()
+
+
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    """(pointer, where) of a uint8 buffer: CUDA tensor -> DEVICE, numpy -> HOST."""
+    if _is_torch(x):
+        import torch
+        if x.dtype != torch.uint8:
+            raise TypeError("expected a uint8 tensor")
+        if not x.is_contiguous():
+            raise ValueError("expected a contiguous tensor")
+        if x.is_cuda:
+            return x.data_ptr(), DEVICE
+        return x.data_ptr(), HOST_PINNED if x.is_pinned() else HOST
+    if isinstance(x, np.ndarray):
+        if x.dtype != np.uint8 or not x.flags["C_CONTIGUOUS"]:
+            raise TypeError("expected a C-contiguous uint8 array")
+        return x.ctypes.data, HOST
+    raise TypeError("unsupported buffer type %r" % type(x))
+
+
+class Codec:
+    """One memo_ec context on one GPU (one per thread, like the reference's
+    background pool threads; elle/src/elle/reactor/scheduler.cc:562-602)."""
+
+    def __init__(self, device=0):
+        self._ctx = ctypes.c_void_p()
+        _check(_lib().memo_ec_ctx_create(device, ctypes.byref(self._ctx)), "ctx_create")
+        self.device = device
+
+    def close(self):
+        if self._ctx:
+            _lib().memo_ec_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- streams
+    def set_stream(self, stream):
+        """Enqueue device work on a torch.cuda.Stream / raw hipStream_t (None = own)."""
+        if stream is None:
+            h = None
+        elif isinstance(stream, int):
+            h = stream
+        else:
+            h = stream.cuda_stream
+        _check(_lib().memo_ec_set_stream(self._ctx, h), "set_stream")
+
+    @property
+    def stream(self):
+        return _lib().memo_ec_get_stream(self._ctx)
+
+    def synchronize(self):
+        _check(_lib().memo_ec_synchronize(self._ctx), "synchronize")
+
+    # -- codec
+    def encode(self, k, m, data, parity, S=None, n=None):
+        """parity (n x m x S) <- data (n x k x S); device (async) or host (sync)."""
+        dp, dw = _ptr(data)
+        pp, pw = _ptr(parity)
+        if (dw == DEVICE) != (pw == DEVICE):
+            raise ValueError("data and parity must both be device or both host buffers")
+        if S is None:
+            n, S = _infer_nS(data, k)
+        where = DEVICE if dw == DEVICE else (HOST_PINNED if dw == pw == HOST_PINNED else HOST)
+        _check(_lib().memo_ec_encode_batch(self._ctx, k, m, S, n, dp, pp, where), "encode")
+        return parity
+
+    def rebuild(self, k, m, surv_idx, surv, lost_idx, out, S=None, n=None):
+        """out (n x e x S) <- the k survivor shards surv (n x k x S) of each block."""
+        sp, sw = _ptr(surv)
+        op, ow = _ptr(out)
+        ip, iw = _ptr(surv_idx)
+        lp, lw = _ptr(lost_idx)
+        if S is None:
+            n, S = _infer_nS(surv, k)
+        e = lost_idx.shape[1] if len(lost_idx.shape) == 2 else 0
+        if sw == DEVICE:
+            if not (ow == iw == lw == DEVICE):
+                raise ValueError("device rebuild needs every buffer on the device")
+            where = DEVICE
+        else:
+            if DEVICE in (ow, iw, lw):
+                raise ValueError("host rebuild needs every buffer in host memory")
+            where = HOST_PINNED if sw == ow == HOST_PINNED else HOST
+        _check(_lib().memo_ec_rebuild_batch(self._ctx, k, m, S, n, ip, sp, lp, e, op, where),
+               "rebuild")
+        return out
+
+    def decode_rows(self, k, m, surv_idx, lost_idx, rows):
+        n, e = lost_idx.shape
+        _check(_lib().memo_ec_decode_rows(self._ctx, k, m, n, _ptr(surv_idx)[0], _ptr(lost_idx)[0],
+                                          e, _ptr(rows)[0]), "decode_rows")
+        return rows
+
+    def encode_segments(self, segs):
+        """segs: list of (k, m, S, n, data_tensor, parity_tensor) on this device."""
+        arr = (Segment * len(segs))()
+        for i, (k, m, S, n, d, p) in enumerate(segs):
+            arr[i] = Segment(k, m, S, n, _ptr(d)[0], _ptr(p)[0])
+        _check(_lib().memo_ec_encode_segments(self._ctx, len(segs), arr), "encode_segments")
+
+    def fill_blocks(self, seed, first_block, n, B, k, S, out):
+        _check(_lib().memo_ec_fill_blocks(self._ctx, seed, first_block, n, B, k, S, _ptr(out)[0]),
+               "fill_blocks")
+        return out
+
+    def gather_shards(self, k, m, S, n, data, parity, idx, out):
+        cnt = idx.shape[1]
+        _check(_lib().memo_ec_gather_shards(self._ctx, k, m, S, n, _ptr(data)[0], _ptr(parity)[0],
+                                            _ptr(idx)[0], cnt, _ptr(out)[0]), "gather_shards")
+        return out
+
+
+def _infer_nS(buf, k):
+    shape = tuple(buf.shape)
+    if len(shape) == 3:
+        return shape[0], shape[2]
+    if len(shape) == 2:
+        if shape[1] % k:
+            raise ValueError("row length not a multiple of k")
+        return shape[0], shape[1] // k
+    raise ValueError("pass S and n for a flat buffer")

@@ -1,0 +1,69 @@
+"""C-ABI library checks that need no GPU: it loads, exports every symbol
+include/memo_ec.h declares, and its host-only functions agree with the
+oracle.  No compute call is made here."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, SEED
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "memo_ec.h")).read()
+    return sorted(set(re.findall(r"\b(memo_ec_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    from memo_amd import ec
+    assert sorted(ec.EXPORTS) == header_symbols()
+
+
+def test_library_exports_every_header_symbol():
+    from memo_amd import ec
+    lib = ctypes.CDLL(ec.LIB_PATH)
+    for name in header_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_library_is_gfx950_code():
+    from memo_amd import ec
+    blob = open(ec.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_host_functions_match_oracle(O):
+    from memo_amd import ec
+    for B in [0, 1, 63, 64, 1000, 65536, 1 << 20, 4 << 20]:
+        for k in [3, 4, 10, 16]:
+            assert ec.shard_size(B, k) == O.shard_size(B, k)
+    for (k, m) in [(3, 2), (4, 2), (10, 4), (16, 4), (64, 16)]:
+        assert np.array_equal(ec.generator(k, m), O.cauchy(k, m))
+    for (k, m, e) in [(3, 2, 2), (10, 4, 4), (16, 4, 1), (4, 2, 0)]:
+        s, l = ec.erasures(SEED, 17, 50, k, m, e)
+        so, lo = O.erasures(SEED, 17, 50, k, m, e)
+        assert np.array_equal(s, so) and np.array_equal(l, lo)
+
+
+def test_error_codes_and_limits():
+    from memo_amd import ec
+    L = ec._lib()
+    assert L.memo_ec_version() == 1
+    assert L.memo_ec_strerror(-4) == b"survivor shards cannot rebuild the block"
+    with pytest.raises(ec.MemoECError):
+        ec.generator(65, 4)
+    with pytest.raises(ec.MemoECError):
+        ec.generator(0, 4)
+    c = ctypes.c_void_p()
+    assert L.memo_ec_encode_batch(None, 10, 4, 64, 1, None, None, 2) == -1
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from memo_amd import ec
+    with pytest.raises(ec.MemoECError):
+        ec.Codec(0)

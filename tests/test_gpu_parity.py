@@ -1,0 +1,224 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and
+the golden fixtures, bit-exact.  Full-size configs (BASELINE.json C2/C3)
+are checked through size-independent properties (rebuild round trips,
+sampled blocks against the oracle)."""
+import itertools
+
+import numpy as np
+import pytest
+
+from conftest import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def empty(*shape):
+    import torch
+    return torch.empty(shape, dtype=torch.uint8, device="cuda")
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def fill(codec, fb, n, B, k, S):
+    d = empty(n, k * S)
+    codec.fill_blocks(SEED, fb, n, B, k, S, d)
+    return d
+
+
+def test_fill_matches_oracle(codec, O):
+    for (B, k) in [(0, 3), (1, 3), (7, 4), (1000, 3), (4095, 4), (5000, 10), (1 << 16, 16)]:
+        S = O.shard_size(B, k)
+        d = fill(codec, 3, 5, B, k, S)
+        codec.synchronize()
+        assert np.array_equal(host(d), O.fill_blocks(SEED, 3, 5, B, k, S)), (B, k)
+
+
+def test_golden_cases(codec, golden, O):
+    for ci, row in enumerate(golden["cases"]):
+        k, m, B, fb, nb, e, S = map(int, row)
+        d = fill(codec, fb, nb, B, k, S)
+        p = empty(nb, m * S)
+        codec.encode(k, m, d, p)
+        codec.synchronize()
+        assert np.array_equal(host(p), golden["case%d_parity" % ci]), ci
+        s, l = dev(golden["case%d_surv" % ci]), dev(golden["case%d_lost" % ci])
+        rows = empty(nb, e * k)
+        codec.decode_rows(k, m, s, l, rows)
+        codec.synchronize()
+        assert np.array_equal(host(rows).reshape(nb, e, k), golden["case%d_rows" % ci]), ci
+        surv = empty(nb, k * S)
+        codec.gather_shards(k, m, S, nb, d, p, s, surv)
+        out = empty(nb, e * S)
+        codec.rebuild(k, m, s, surv, l, out)
+        want = empty(nb, e * S)
+        codec.gather_shards(k, m, S, nb, d, p, l, want)
+        codec.synchronize()
+        assert np.array_equal(host(out), host(want)), ci
+
+
+CONFIGS = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (6, 6), (8, 5), (10, 4), (12, 7), (16, 4),
+           (20, 8), (33, 12), (64, 16)]
+
+
+@pytest.mark.parametrize("k,m", CONFIGS)
+def test_encode_rebuild_vs_oracle(codec, O, k, m):
+    rng = np.random.default_rng(k * 100 + m)
+    for B in [64 * k, 4096, 12345, 300000]:
+        S = O.shard_size(B, k)
+        n = int(rng.integers(1, 9))
+        fb = int(rng.integers(0, 1000))
+        d = fill(codec, fb, n, B, k, S)
+        p = empty(n, m * S)
+        codec.encode(k, m, d, p)
+        data = O.fill_blocks(SEED, fb, n, B, k, S)
+        want = O.encode(k, m, S, data)
+        codec.synchronize()
+        assert np.array_equal(host(p), want), (k, m, B)
+        for e in sorted({1, m}):
+            s, l = O.erasures(SEED, fb, n, k, m, e)
+            surv = O.gather(k, m, S, data, want, s)
+            out = empty(n, e * S)
+            codec.rebuild(k, m, dev(s), dev(surv), dev(l), out)
+            codec.synchronize()
+            assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2)])
+def test_every_erasure_pattern_in_one_batch(codec, O, k, m):
+    """Each block of the batch has a different erasure pattern (per-block
+    decode tables in one launch); all patterns of size m."""
+    pats = list(itertools.combinations(range(k + m), m))
+    n, B = len(pats), 3000
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    lost = np.array(pats, dtype=np.uint8)
+    surv = np.array([[i for i in range(k + m) if i not in p][:k] for p in pats], dtype=np.uint8)
+    sv = O.gather(k, m, S, data, par, surv)
+    out = empty(n, m * S)
+    codec.rebuild(k, m, dev(surv), dev(sv), dev(lost), out)
+    codec.synchronize()
+    assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost))
+
+
+def test_small_blocks_many_per_tile(codec, O):
+    # 4 KiB blocks with k=16: S=256, 16 columns per block, tables for ~17
+    # blocks per tile in the rebuild kernel.
+    k, m, B, n = 16, 4, 4096, 300
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 40, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    d = dev(data)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    s, l = O.erasures(SEED, 40, n, k, m, 4)
+    out = empty(n, 4 * S)
+    codec.rebuild(k, m, dev(s), dev(O.gather(k, m, S, data, par, s)), dev(l), out)
+    codec.synchronize()
+    assert np.array_equal(host(p), par)
+    assert np.array_equal(host(out), O.gather(k, m, S, data, par, l))
+
+
+def test_mixed_segments_one_launch(codec, O):
+    segs, want = [], []
+    for i, (k, m, B, n) in enumerate([(4, 2, 4096, 37), (10, 4, 1 << 20, 3), (16, 4, 65536, 11),
+                                      (10, 4, 16384, 20), (4, 2, 4 << 20, 1)]):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 100 * i, n, B, k, S)
+        p = empty(n, m * S)
+        segs.append((k, m, S, n, dev(data), p))
+        want.append(O.encode(k, m, S, data))
+    codec.encode_segments(segs)
+    codec.synchronize()
+    for (k, m, S, n, d, p), w in zip(segs, want):
+        assert np.array_equal(host(p), w), (k, m, S)
+
+
+def test_host_memory_paths(codec, O):
+    import torch
+    k, m, B, n = 10, 4, 1 << 20, 70  # > one 64 MiB pipeline batch
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 5, n, B, k, S)
+    want = O.encode(k, m, S, data)
+    par = np.zeros((n, m * S), np.uint8)
+    codec.encode(k, m, data, par)                       # pageable
+    assert np.array_equal(par, want)
+    pd = torch.from_numpy(data).pin_memory()
+    pp = torch.zeros((n, m * S), dtype=torch.uint8).pin_memory()
+    codec.encode(k, m, pd, pp)                          # pinned
+    assert np.array_equal(pp.numpy(), want)
+    s, l = O.erasures(SEED, 5, n, k, m, 3)
+    surv = O.gather(k, m, S, data, want, s)
+    out = np.zeros((n, 3 * S), np.uint8)
+    codec.rebuild(k, m, s, surv, l, out)
+    assert np.array_equal(out, O.gather(k, m, S, data, want, l))
+
+
+def test_singular_survivors_reported(codec):
+    from memo_amd import ec
+    k, m, S, n = 4, 2, 64, 2
+    surv = dev(np.array([[0, 1, 2, 3], [0, 1, 1, 2]], np.uint8))  # block 1: duplicate
+    lost = dev(np.array([[4], [3]], np.uint8))
+    out = empty(n, S)
+    codec.rebuild(k, m, surv, empty(n, k * S).zero_(), lost, out)
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.synchronize()
+    assert ei.value.code == -4
+    codec.synchronize()  # error is cleared
+
+
+def test_noops_and_argument_errors(codec):
+    from memo_amd import ec
+    d = empty(1, 10 * 64)
+    codec.encode(10, 4, d, empty(0), S=64, n=0)
+    with pytest.raises(ec.MemoECError):
+        codec.encode(10, 4, d, empty(1, 4 * 64), S=48, n=1)   # S not a multiple of 64
+    with pytest.raises(ec.MemoECError):
+        codec.encode(65, 4, d, empty(1, 4 * 64), S=64, n=1)   # k beyond limit
+    codec.synchronize()
+
+
+def test_full_size_c2_c3_round_trip(codec, O):
+    """BASELINE.json C2/C3 at full size (4096 x 1 MiB, RS(10,4), e=4):
+    sampled blocks bit-exact vs the oracle; every block's 4 erased shards
+    rebuilt bit-exact (device-side comparison)."""
+    import torch
+    k, m, B, n, e = 10, 4, 1 << 20, 4096, 4
+    S = O.shard_size(B, k)
+    d = fill(codec, 0, n, B, k, S)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    codec.synchronize()
+    for b in [0, 1, 777, 2048, n - 1]:
+        data = O.fill_blocks(SEED, b, 1, B, k, S)
+        assert np.array_equal(host(p[b:b + 1]), O.encode(k, m, S, data)), b
+    s, l = ec_erasures(n, k, m, e)
+    sd, ld = dev(s), dev(l)
+    surv = empty(n, k * S)
+    codec.gather_shards(k, m, S, n, d, p, sd, surv)
+    out = empty(n, e * S)
+    codec.rebuild(k, m, sd, surv, ld, out)
+    want = empty(n, e * S)
+    codec.gather_shards(k, m, S, n, d, p, ld, want)
+    codec.synchronize()
+    assert torch.equal(out, want)
+    del surv, want
+    # data shards alone (lost = all parity) re-encode identically
+    lp = dev(np.tile(np.arange(k, k + m, dtype=np.uint8), (n, 1)))
+    sp = dev(np.tile(np.arange(k, dtype=np.uint8), (n, 1)))
+    out2 = empty(n, m * S)
+    codec.rebuild(k, m, sp, d, lp, out2)
+    codec.synchronize()
+    assert torch.equal(out2, p)
+
+
+def ec_erasures(n, k, m, e):
+    from memo_amd import ec
+    return ec.erasures(SEED, 0, n, k, m, e)

@@ -1,0 +1,126 @@
+"""CPU oracle checks: published GF(2^8)/0x11D values, golden fixtures from
+the independent numpy restatement, and codec properties."""
+import hashlib
+import itertools
+
+import numpy as np
+import pytest
+
+from conftest import SEED
+
+# ISO/IEC 18004 (QR code) antilog table for x^8+x^4+x^3+x^2+1, first 30 values.
+QR_EXP = [1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38, 76, 152, 45, 90,
+          180, 117, 234, 201, 143, 3, 6, 12, 24, 48]
+# Published QR "HELLO WORLD" version 1-M: 16 data codewords -> 10 EC codewords.
+QR_DATA = [32, 91, 11, 120, 209, 114, 220, 77, 67, 64, 236, 17, 236, 17, 236, 17]
+QR_EC = [196, 35, 39, 119, 235, 215, 231, 226, 93, 23]
+
+
+def test_field_published_values(O):
+    assert [O.gf_exp(i) for i in range(30)] == QR_EXP
+    assert O.gf_exp(255) == 1
+    for a in range(1, 256):
+        assert O.gf_mul(a, O.gf_inv(a)) == 1
+    assert O.gf_mul(0x53, 0xCA) == 0x8F
+
+
+def test_field_qr_hello_world(O):
+    g = [1]
+    for i in range(10):
+        a = O.gf_exp(i)
+        ng = [0] * (len(g) + 1)
+        for j, c in enumerate(g):
+            ng[j] ^= c
+            ng[j + 1] ^= O.gf_mul(c, a)
+        g = ng
+    msg = QR_DATA + [0] * 10
+    for i in range(len(QR_DATA)):
+        c = msg[i]
+        if c:
+            for j in range(1, len(g)):
+                msg[i + j] ^= O.gf_mul(g[j], c)
+    assert msg[len(QR_DATA):] == QR_EC
+
+
+def test_survey_self_checks(O):
+    C = O.cauchy(3, 2)
+    assert C[3:].tobytes().hex() == "f48e0147a77a"
+    assert O.cauchy(10, 4)[10].tobytes().hex() == "dd98ad9d5d963daa8ef4"
+    for (k, m, want) in [(3, 2, "7b9a"), (10, 4, "5353c9c9"), (16, 4, "1f1f1f1f")]:
+        p = O.encode(k, m, 64, np.ones((1, k * 64), np.uint8))
+        assert p[0, ::64].tobytes().hex() == want
+
+
+def test_generators_match_golden(O, golden):
+    for (k, m) in [(3, 2), (4, 2), (10, 4), (16, 4)]:
+        assert np.array_equal(O.cauchy(k, m), golden["gen_%d_%d" % (k, m)])
+    assert np.array_equal(np.array([O.gf_exp(i) for i in range(255)], np.uint8), golden["gf_exp"])
+
+
+def test_encode_rebuild_match_golden(O, golden):
+    for ci, (k, m, B, fb, nb, e, S) in enumerate(golden["cases"]):
+        k, m, B, fb, nb, e, S = map(int, (k, m, B, fb, nb, e, S))
+        assert O.shard_size(B, k) == S
+        data = O.fill_blocks(SEED, fb, nb, B, k, S)
+        assert hashlib.sha256(data.tobytes()).digest() == golden["case%d_data_sha256" % ci].tobytes()
+        par = O.encode(k, m, S, data)
+        assert np.array_equal(par, golden["case%d_parity" % ci]), ci
+        s, l = O.erasures(SEED, fb, nb, k, m, e)
+        assert np.array_equal(s, golden["case%d_surv" % ci])
+        assert np.array_equal(l, golden["case%d_lost" % ci])
+        for b in range(nb):
+            assert np.array_equal(O.decode_matrix(k, m, s[b], l[b]), golden["case%d_rows" % ci][b])
+        surv = O.gather(k, m, S, data, par, s)
+        want = O.gather(k, m, S, data, par, l)
+        assert np.array_equal(O.rebuild(k, m, S, s, surv, l), want)
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2)])
+def test_exhaustive_erasure_patterns(O, golden, k, m):
+    lost_all = golden["exh_%d_%d_lost" % (k, m)]
+    rows_all = golden["exh_%d_%d_rows" % (k, m)]
+    S = 64
+    data = O.fill_blocks(SEED, 11, 1, k * S, k, S)
+    par = O.encode(k, m, S, data)
+    full = np.concatenate([data.reshape(k, S), par.reshape(m, S)])
+    for lp, want_rows in zip(lost_all, rows_all):
+        lost = [int(x) for x in lp if x != 255]
+        e = len(lost)
+        surv = [i for i in range(k + m) if i not in lost][:k]
+        assert np.array_equal(O.decode_matrix(k, m, surv, lost), want_rows[:e])
+        out = O.rebuild(k, m, S, np.array([surv]), full[surv].reshape(1, -1), np.array([lost]))
+        assert np.array_equal(out.reshape(e, S), full[lost])
+
+
+def test_properties(O):
+    k, m, S = 10, 4, 256
+    a = O.fill_blocks(SEED, 1, 2, k * S, k, S)
+    b = O.fill_blocks(SEED, 2, 2, k * S, k, S)
+    # zero data -> zero parity; linearity; systematic identity
+    assert not O.encode(k, m, S, np.zeros_like(a)).any()
+    assert np.array_equal(O.encode(k, m, S, a ^ b), O.encode(k, m, S, a) ^ O.encode(k, m, S, b))
+    C = O.cauchy(k, m)
+    assert np.array_equal(C[:k], np.eye(k, dtype=np.uint8))
+    # MDS: every k-subset of rows is invertible (sampled)
+    rng = np.random.default_rng(0)
+    for _ in range(200):
+        rows = sorted(rng.choice(k + m, k, replace=False))
+        inv = O.invert(C[rows])
+        from oracle import rs_numpy as N
+        assert np.array_equal(N.matmul(C[rows], inv), np.eye(k, dtype=np.uint8))
+
+
+def test_threaded_baseline_matches_scalar(O):
+    k, m, B = 10, 4, 100000
+    S = O.shard_size(B, k)
+    d = O.fill_blocks(SEED, 0, 9, B, k, S)
+    assert np.array_equal(O.encode(k, m, S, d, threads=4), O.encode(k, m, S, d))
+    s, l = O.erasures(SEED, 0, 9, k, m, 4)
+    p = O.encode(k, m, S, d)
+    surv = O.gather(k, m, S, d, p, s)
+    assert np.array_equal(O.rebuild(k, m, S, s, surv, l, threads=3), O.gather(k, m, S, d, p, l))
+
+
+def test_singular_survivors_rejected(O):
+    with pytest.raises(ValueError):
+        O.decode_matrix(4, 2, [0, 1, 1, 2], [3])
