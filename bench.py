@@ -135,9 +135,13 @@ def main():
 
     k, m, B, n, e = args.k, args.m, args.block_bytes, args.blocks, args.erasures
     S = ec.shard_size(B, k)
-    stream = torch.cuda.current_stream()
+    # A dedicated (non-null) stream: the codec enqueues on it and the HIP
+    # events that time each launch are recorded on the same stream.
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     codec = ec.Codec(local if world > 1 else 0)
     codec.set_stream(stream)
+    assert codec.stream == stream.cuda_stream and stream.cuda_stream
 
     data = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
     par = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")

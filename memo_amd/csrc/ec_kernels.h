@@ -6,30 +6,45 @@
 
 #include "../../include/memo_ec.h"
 
+#ifndef MEMO_EC_MAC_NT
+#define MEMO_EC_MAC_NT 1
+#endif
+#ifndef MEMO_EC_MAC_TABFIRST
+#define MEMO_EC_MAC_TABFIRST 1
+#endif
+#ifndef MEMO_EC_MAC_WAVES
+#define MEMO_EC_MAC_WAVES 1
+#endif
+#ifndef MEMO_EC_MAC_PAIR
+#define MEMO_EC_MAC_PAIR 1
+#endif
+
 namespace memo_ec {
 
-// Columns (16-byte units) per lane per tile; a tile is 256 * MAC_V units.
-constexpr int MAC_V = 1;
-constexpr uint32_t MAC_UNITS = 256 * MAC_V;
-// Streamed shard loads / parity stores bypass cache retention (read once).
-constexpr bool MAC_NT = true;
+// Streamed shard loads / output stores are non-temporal (read/written once).
+constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
+// Fold shards pairwise (three 3-input XORs per 2 coefficients).
+constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
+// Table dwords per lane staged through registers ahead of the shard loads.
+constexpr int MAC_TAB_REGS = 2;
+// A tile = 256 16-byte columns = one workgroup of gf_mac_kernel.
+constexpr uint32_t MAC_TILE = 256;
 
 // One (kin -> r) multiply-accumulate over n blocks.
 struct MacSeg {
   const uint8_t* in;      // block b, input shard j at in + b*in_bstride + j*in_sstride
   uint8_t* out;           // block b, output shard i at out + b*out_bstride + i*out_sstride
-  const uint8_t* coef;    // r x kin per block (coef_bstride apart); nullptr = Cauchy parity rows
+  const uint32_t* tab;    // product-table image(s): R x kpad coefficients x 8 dwords
   uint64_t in_bstride, in_sstride;
   uint64_t out_bstride, out_sstride;
-  uint64_t coef_bstride;
+  uint64_t tab_bstride;   // dwords between blocks' images; 0 = one image for all
   uint64_t n;             // blocks
-  uint64_t tiles;         // work tiles of this segment
+  uint64_t tiles;         // tiles (= workgroups) of this segment
   uint64_t tiles_per_block;  // aligned mapping only
   uint32_t chunks;        // C = S / 16
-  uint32_t kin, r;
+  uint32_t kin, r, kpad;
   uint32_t flat;          // 1: flattened (block, column) units; 0: tile inside one block
   uint32_t wg_begin;      // first workgroup of this segment
-  uint32_t wgs;           // workgroups of this segment (contiguous tile ranges)
 };
 
 struct MacLaunch {
@@ -41,10 +56,11 @@ struct MacLaunch {
 struct DecodeArgs {
   const uint8_t* surv_idx;
   const uint8_t* lost_idx;
-  uint8_t* rows;
+  uint8_t* rows;          // n x e x k decode rows (optional)
+  uint32_t* tab;          // n x (R x kpad x 8) product-table images (optional)
   uint32_t* status;
   uint64_t n;
-  uint32_t k, m, e;
+  uint32_t k, m, e, R, kpad;
 };
 
 struct FillArgs {
@@ -65,7 +81,9 @@ struct GatherArgs {
 // (shards beyond kin inside the last chunk are zero) used for (kin, r).
 int mac_rbound(int r);
 int mac_kchunk(int kin);
-hipError_t launch_mac(int KC, int R, bool shared, const MacLaunch& L, uint32_t grid, size_t lds,
+void table_image_host(const uint8_t* coef, uint32_t r, uint32_t kin, uint32_t R, uint32_t kpad,
+                      uint32_t* out);
+hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t lds,
                       hipStream_t st);
 hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);

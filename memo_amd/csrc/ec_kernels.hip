@@ -2,25 +2,29 @@
 //
 // Hot path: gf_mac_kernel, the batched GF(2^8) multiply-accumulate
 //   out[b][i][x] = XOR_j coef_b[i][j] * in[b][j][x]
-// that is RS encode (coef = the Cauchy parity rows, shared by every block)
+// which is RS encode (coef = the Cauchy parity rows, shared by every block)
 // and RS rebuild (coef = per-block decode rows from decode_rows_kernel).
 // It replaces the replication byte movement of Paxos::Details::
 // send_immutable_block / _fetch / _rebalance (src/memo/model/doughnut/
 // consensus/Paxos.cc:315-391, 486-519, 1012-1246); see DESIGN.md.
 //
-// Design:
-//  * HBM-bound streaming: each lane owns 16-byte columns of a block and loads
-//    the same 16 bytes of every input shard (dwordx4, a wave reads 1 KiB of
-//    one shard per instruction, fully coalesced), G shards x V columns in
-//    flight per lane, double-buffered.
+// Design, measured on MI355X (tools/hbm_probe.hip):
+//  * HBM-bound streaming.  One workgroup = one tile of 256 16-byte columns;
+//    each lane loads the same 16 bytes of every input shard (dwordx4: a wave
+//    reads 1 KiB of one shard per instruction, fully coalesced) and stores
+//    16 bytes of every output shard, non-temporal.  One tile per workgroup
+//    and a grid of all tiles beat persistent/grid-stride loops (the shard
+//    pattern probe: 5.69 TB/s at 1 unit/lane vs 5.26 at 8).
+//  * The kin loads are issued before anything else; the workgroup copies its
+//    product tables (global image -> LDS) while they are in flight.
 //  * Byte-field GF multiply on the VALU, no MFMA: a data byte x is split into
 //    3+3+2-bit fields (x>>5, (x>>2)&7, x&3); c*x = T_hi[x>>5] ^ T_mid[(x>>2)&7]
 //    ^ T_lo[x&3].  Each table has <= 8 byte entries, so one v_perm_b32 looks
-//    up 4 bytes at once; 3 perms + 3-input XORs (v_bitop3_b32) per
-//    coefficient per dword.  The field selectors are shared by all outputs.
-//  * The GF log/antilog tables and the per-coefficient product tables are
-//    staged in LDS at workgroup start (tables read back as wave-broadcast
-//    ds_read_b128/b32).
+//    up 4 bytes at once: 3 perms + 1.5 v_bitop3_b32 (3-input XOR) per
+//    coefficient per dword; the field selectors are shared by all outputs.
+//  * The GF log/antilog tables live in LDS in decode_rows_kernel (batched
+//    Gauss-Jordan inversion), which also emits the per-block product-table
+//    images the rebuild MAC consumes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -51,12 +55,12 @@ constexpr GfTables make_gf() {
 __constant__ GfTables kGf = make_gf();
 const GfTables kGfHost = make_gf();
 
-__device__ __forceinline__ uint32_t gf_mul_lds(const uint8_t* lg, const uint8_t* ex,
-                                               uint32_t a, uint32_t b) {
+__host__ __device__ __forceinline__ uint32_t gf_mul_t(const uint8_t* lg, const uint8_t* ex,
+                                                      uint32_t a, uint32_t b) {
   return (a && b) ? ex[lg[a] + lg[b]] : 0u;
 }
-__device__ __forceinline__ uint32_t gf_inv_lds(const uint8_t* lg, const uint8_t* ex,
-                                               uint32_t a) {
+__host__ __device__ __forceinline__ uint32_t gf_inv_t(const uint8_t* lg, const uint8_t* ex,
+                                                      uint32_t a) {
   return a ? ex[255 - lg[a]] : 0u;
 }
 
@@ -66,52 +70,37 @@ __device__ __forceinline__ void stage_gf(uint32_t* s_gf) {
   for (int i = threadIdx.x; i < 192; i += blockDim.x) s_gf[i] = src[i];
 }
 
-// Coefficient of output row i, input column j of segment `sg` for block b.
-__device__ __forceinline__ uint32_t seg_coef(const MacSeg& sg, const uint8_t* lg,
-                                             const uint8_t* ex, uint64_t b, uint32_t i,
-                                             uint32_t j) {
-  if (sg.coef == nullptr)  // systematic Cauchy parity rows: 1 / ((kin+i) ^ j)
-    return gf_inv_lds(lg, ex, (sg.kin + i) ^ j);
-  return sg.coef[b * sg.coef_bstride + (uint64_t)i * sg.kin + j];
-}
-
-// Product-table dword q of coefficient c (layout per coefficient: 8 dwords,
-// [mid0 mid1 hi0 hi1 lo - - -]; each dword packs 4 byte entries).
-__device__ __forceinline__ uint32_t table_dword(const uint8_t* lg, const uint8_t* ex,
-                                                uint32_t c, uint32_t q) {
+// Product-table dword q of coefficient c.  Image per coefficient: 8 dwords
+// [mid0 mid1 hi0 hi1 lo 0 0 0], each dword packing 4 byte entries:
+//   mid0/mid1: c*(v<<2), v = 0..3 / 4..7;  hi0/hi1: c*(v<<5);  lo: c*v, v<4.
+__host__ __device__ __forceinline__ uint32_t table_dword(const uint8_t* lg, const uint8_t* ex,
+                                                         uint32_t c, uint32_t q) {
   uint32_t r = 0;
-#pragma unroll
   for (uint32_t e = 0; e < 4; ++e) {
     uint32_t x;
     switch (q) {
-      case 0: x = e << 2; break;        // mid entries 0..3
-      case 1: x = (e + 4) << 2; break;  // mid entries 4..7
-      case 2: x = e << 5; break;        // hi entries 0..3
-      case 3: x = (e + 4) << 5; break;  // hi entries 4..7
-      default: x = e; break;            // lo entries 0..3
+      case 0: x = e << 2; break;
+      case 1: x = (e + 4) << 2; break;
+      case 2: x = e << 5; break;
+      case 3: x = (e + 4) << 5; break;
+      case 4: x = e; break;
+      default: return 0;
     }
-    r |= gf_mul_lds(lg, ex, c, x) << (8 * e);
+    r |= gf_mul_t(lg, ex, c, x) << (8 * e);
   }
   return r;
 }
 
-// Build nsets x R x kpad coefficient tables for blocks [b_first, b_first+nsets).
-// Rows i >= r and columns j >= kin get coefficient 0, i.e. all-zero tables,
-// so padded shards contribute nothing whatever bytes their registers hold.
-__device__ __forceinline__ void build_tables(const MacSeg& sg, uint32_t* s_tab, const uint8_t* lg,
-                                             const uint8_t* ex, uint64_t b_first, uint32_t nsets,
-                                             uint32_t R, uint32_t kpad) {
-  const uint32_t per_set = R * kpad;
-  const uint32_t total = nsets * per_set * 5;
-  for (uint32_t t = threadIdx.x; t < total; t += blockDim.x) {
-    const uint32_t q = t % 5;
-    const uint32_t cidx = t / 5;
-    const uint32_t set = cidx / per_set;
-    const uint32_t rem = cidx - set * per_set;
-    const uint32_t i = rem / kpad, j = rem - i * kpad;
-    const uint32_t c = (i < sg.r && j < sg.kin) ? seg_coef(sg, lg, ex, b_first + set, i, j) : 0u;
-    s_tab[cidx * 8 + q] = table_dword(lg, ex, c, q);
-  }
+// Host: table image (R x kpad coefficients, 8 dwords each) of an r x kin
+// coefficient matrix; rows >= r and columns >= kin are zero coefficients.
+void table_image_host(const uint8_t* coef, uint32_t r, uint32_t kin, uint32_t R, uint32_t kpad,
+                      uint32_t* out) {
+  for (uint32_t i = 0; i < R; ++i)
+    for (uint32_t j = 0; j < kpad; ++j) {
+      const uint32_t c = (i < r && j < kin) ? coef[i * kin + j] : 0u;
+      for (uint32_t q = 0; q < 8; ++q)
+        out[(i * kpad + j) * 8 + q] = table_dword(kGfHost.log, kGfHost.exp, c, q);
+    }
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -136,7 +125,7 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
-// acc ^= coef * x for 4 dwords (16 bytes).
+// Field selectors of 4 data bytes (shared by every output row).
 struct Sel {
   uint32_t lo, mid, hi;
 };
@@ -157,202 +146,206 @@ __device__ __forceinline__ Tab read_tab(const uint32_t* tp) {
 }
 __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl, uint32_t& pm,
                                         uint32_t& ph) {
+#ifdef MEMO_EC_MAC_XORONLY  // diagnostic build: no GF math (wrong results)
+  pl = s.lo ^ t.lo; pm = s.mid; ph = s.hi;
+#else
   pl = __builtin_amdgcn_perm(t.lo, t.lo, s.lo);
   pm = __builtin_amdgcn_perm(t.m1, t.m0, s.mid);
   ph = __builtin_amdgcn_perm(t.h1, t.h0, s.hi);
+#endif
 }
 
 // acc[i] ^= coef(i, j0 + g) * d[g] for the KC shards of one chunk.  Shards
 // are taken in pairs so that 6 partial products + the accumulator fold with
-// three 3-input XORs (v_bitop3_b32: 1.5 per coefficient).  Branch-free:
-// padded rows/shards have all-zero tables.
-template <int KC, int R, int V>
-__device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][V][4], const uint4 (&d)[KC][V],
-                                          const uint32_t* const (&tabv)[V], uint32_t kpad,
-                                          uint32_t j0) {
+// three 3-input XORs.  Branch-free: padded rows/shards have all-zero tables.
+template <int KC, int R>
+__device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
+                                          const uint32_t* tab, uint32_t kpad, uint32_t j0) {
 #pragma unroll
-  for (int g = 0; g < KC; g += 2) {
-    constexpr int dummy = 0;
-    (void)dummy;
-    const bool two = g + 1 < KC;
-    Sel sa[V][4], sb[V][4];
-#pragma unroll
-    for (int v = 0; v < V; ++v) {
-      sa[v][0] = make_sel(d[g][v].x);
-      sa[v][1] = make_sel(d[g][v].y);
-      sa[v][2] = make_sel(d[g][v].z);
-      sa[v][3] = make_sel(d[g][v].w);
-      if (two) {
-        sb[v][0] = make_sel(d[g + 1][v].x);
-        sb[v][1] = make_sel(d[g + 1][v].y);
-        sb[v][2] = make_sel(d[g + 1][v].z);
-        sb[v][3] = make_sel(d[g + 1][v].w);
-      }
+  for (int g = 0; g < KC; g += MAC_PAIR ? 2 : 1) {
+    const bool two = MAC_PAIR && g + 1 < KC;
+    Sel sa[4], sb[4];
+    sa[0] = make_sel(d[g].x);
+    sa[1] = make_sel(d[g].y);
+    sa[2] = make_sel(d[g].z);
+    sa[3] = make_sel(d[g].w);
+    if (two) {
+      sb[0] = make_sel(d[g + 1].x);
+      sb[1] = make_sel(d[g + 1].y);
+      sb[2] = make_sel(d[g + 1].z);
+      sb[3] = make_sel(d[g + 1].w);
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
+      const uint32_t* tp = tab + (i * kpad + j0 + g) * 8;
+      const Tab ta = read_tab(tp);
+      if (two) {
+        const Tab tb = read_tab(tp + 8);
 #pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const uint32_t* tp = tabv[v] + (i * kpad + j0 + g) * 8;
-        const Tab ta = read_tab(tp);
-        if (two) {
-          const Tab tb = read_tab(tp + 8);
+        for (int w = 0; w < 4; ++w) {
+          uint32_t al, am, ah, bl, bm, bh;
+          lookups(sa[w], ta, al, am, ah);
+          lookups(sb[w], tb, bl, bm, bh);
+          const uint32_t x = xor3(acc[i][w], al, am);
+          const uint32_t y = xor3(ah, bl, bm);
+          acc[i][w] = xor3(x, y, bh);
+        }
+      } else {
 #pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            uint32_t al, am, ah, bl, bm, bh;
-            lookups(sa[v][w], ta, al, am, ah);
-            lookups(sb[v][w], tb, bl, bm, bh);
-            const uint32_t x = xor3(acc[i][v][w], al, am);
-            const uint32_t y = xor3(ah, bl, bm);
-            acc[i][v][w] = xor3(x, y, bh);
-          }
-        } else {
-#pragma unroll
-          for (int w = 0; w < 4; ++w) {
-            uint32_t al, am, ah;
-            lookups(sa[v][w], ta, al, am, ah);
-            acc[i][v][w] = xor3(acc[i][v][w], al, am) ^ ah;
-          }
+        for (int w = 0; w < 4; ++w) {
+          uint32_t al, am, ah;
+          lookups(sa[w], ta, al, am, ah);
+          acc[i][w] = xor3(acc[i][w], al, am) ^ ah;
         }
       }
     }
   }
 }
 
-// One work tile of 256*V column-units; unit = one 16-byte column of one
-// block.  `flat`: units numbered across blocks (u = b*C + c); otherwise a
-// tile lies inside one block (tiles_per_block tiles per block).
-template <int KC, int R, int V, bool SHARED, bool NT>
-__device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, const uint32_t* s_tab,
-                                         uint64_t b_first, uint32_t kpad) {
+// Block/column of this lane in tile `tile` of segment `sg`.
+struct Unit {
+  uint64_t b_first;  // first block of the tile (table set 0)
+  uint32_t nsets;    // blocks touched by the tile
+  uint32_t set;      // this lane's block - b_first
+  bool valid;
+  const uint8_t* pin;
+  uint8_t* pout;
+};
+
+__device__ __forceinline__ Unit locate(const MacSeg& sg, uint64_t tile) {
+  Unit u;
   const uint32_t tid = threadIdx.x;
   const uint32_t C = sg.chunks;
-  const uint32_t kin = sg.kin;
-  const uint64_t total = sg.n * (uint64_t)C;
-
-  const uint8_t* pin[V];
-  uint8_t* pout[V];
-  bool valid[V];
-  const uint32_t* tabv[V];
-#pragma unroll
-  for (int v = 0; v < V; ++v) {
-    uint64_t b, c;
-    if (sg.flat) {
-      uint64_t u = tile * (uint64_t)(256 * V) + (uint64_t)v * 256 + tid;
-      valid[v] = u < total;
-      if (!valid[v]) u = total - 1;
-      b = u / C;
-      c = u - b * C;
-    } else {
-      const uint64_t bt = tile / sg.tiles_per_block;
-      const uint64_t t = tile - bt * sg.tiles_per_block;
-      c = t * (uint64_t)(256 * V) + (uint64_t)v * 256 + tid;
-      b = bt;
-      valid[v] = c < C;
-      if (!valid[v]) c = C - 1;
-    }
-    pin[v] = sg.in + b * sg.in_bstride + c * 16;
-    pout[v] = sg.out + b * sg.out_bstride + c * 16;
-    tabv[v] = SHARED ? s_tab : s_tab + (uint32_t)(b - b_first) * (R * kpad * 8);
-  }
-
-  uint32_t acc[R][V][4];
-#pragma unroll
-  for (int i = 0; i < R; ++i)
-#pragma unroll
-    for (int v = 0; v < V; ++v)
-#pragma unroll
-      for (int w = 0; w < 4; ++w) acc[i][v][w] = 0;
-
-  if (kin == KC) {
-    // Hot path (kin specialised): every load unconditional, so the compiler
-    // issues all KC loads up front and waits with counted vmcnt per pair.
-    uint4 d[KC][V];
-#pragma unroll
-    for (int g = 0; g < KC; ++g)
-#pragma unroll
-      for (int v = 0; v < V; ++v) d[g][v] = ld16<NT>(pin[v] + (uint64_t)g * sg.in_sstride);
-    mac_chunk<KC, R, V>(acc, d, tabv, kpad, 0);
+  uint64_t c0;
+  uint64_t b_last;
+  if (sg.flat) {
+    // units numbered across blocks: u = b*C + c; uniform part in scalars
+    const uint64_t total = sg.n * (uint64_t)C;
+    const uint64_t u0 = tile * 256ull;
+    uint64_t u1 = u0 + 255;
+    if (u1 >= total) u1 = total - 1;
+    u.b_first = u0 / C;
+    b_last = u1 / C;
+    c0 = u0 - u.b_first * C;
   } else {
-    for (uint32_t j0 = 0; j0 < kin; j0 += KC) {
-      uint4 d[KC][V];
-#pragma unroll
-      for (int g = 0; g < KC; ++g)
-        if (j0 + g < kin)
-#pragma unroll
-          for (int v = 0; v < V; ++v)
-            d[g][v] = ld16<NT>(pin[v] + (uint64_t)(j0 + g) * sg.in_sstride);
-      mac_chunk<KC, R, V>(acc, d, tabv, kpad, j0);
-    }
+    // a tile lies inside one block
+    u.b_first = b_last = tile / sg.tiles_per_block;
+    c0 = (tile - u.b_first * sg.tiles_per_block) * 256ull;
   }
-
-#pragma unroll
-  for (int i = 0; i < R; ++i) {
-    if ((uint32_t)i < sg.r) {
-#pragma unroll
-      for (int v = 0; v < V; ++v)
-        if (valid[v])
-          st16<NT>(pout[v] + (uint64_t)i * sg.out_sstride,
-                   make_uint4(acc[i][v][0], acc[i][v][1], acc[i][v][2], acc[i][v][3]));
-    }
+  u.nsets = (uint32_t)(b_last - u.b_first) + 1;
+  uint32_t cc = (uint32_t)c0 + tid;  // < C + 256
+  uint32_t bo = 0;
+  if (sg.flat) {
+    bo = cc / C;
+    cc -= bo * C;
+    u.valid = bo < u.nsets;
+  } else {
+    u.valid = cc < C;
   }
+  if (!u.valid) {  // clamp to a real column; nothing is stored
+    bo = 0;
+    cc = (uint32_t)c0 < C ? (uint32_t)c0 : C - 1;
+  }
+  u.set = bo;
+  const uint64_t b = u.b_first + bo;
+  u.pin = sg.in + b * sg.in_bstride + (uint64_t)cc * 16;
+  u.pout = sg.out + b * sg.out_bstride + (uint64_t)cc * 16;
+  return u;
 }
 
-template <int KC, int R, int V, bool SHARED, bool NT>
-__global__ void __launch_bounds__(256) gf_mac_kernel(const MacLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_gf = smem;          // 768 B log/antilog
-  uint32_t* s_tab = smem + 192;   // product tables
-  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
-  const uint8_t* ex = lg + 256;
+// Copy nsets table images (set s = block b_first + s) into LDS.
+__device__ __forceinline__ void stage_tables(const MacSeg& sg, const Unit& u, uint32_t set_dw,
+                                             uint32_t* s_tab) {
+  // shared image (tab_bstride == 0): one set serves every block
+  const uint32_t total = (sg.tab_bstride ? u.nsets : 1u) * set_dw;
+  const uint32_t* src = sg.tab + (sg.tab_bstride ? u.b_first * sg.tab_bstride : 0);
+  for (uint32_t t = threadIdx.x; t < total; t += 256) s_tab[t] = src[t];
+}
 
-  // Segment of this workgroup (uniform).
+// Register-staged table copy for the hot path: up to MAC_TAB_REGS dwords
+// per lane (R*kpad*8*nsets <= 256*MAC_TAB_REGS), the rest copied directly.
+__device__ __forceinline__ void load_tables(const MacSeg& sg, const Unit& u, uint32_t set_dw,
+                                            uint32_t (&tv)[MAC_TAB_REGS]) {
+  const uint32_t total = (sg.tab_bstride ? u.nsets : 1u) * set_dw;
+  const uint32_t* src = sg.tab + (sg.tab_bstride ? u.b_first * sg.tab_bstride : 0);
+#pragma unroll
+  for (int q = 0; q < MAC_TAB_REGS; ++q) {
+    const uint32_t t = threadIdx.x + 256u * q;
+    tv[q] = t < total ? src[t] : 0u;
+  }
+}
+__device__ __forceinline__ void store_tables(const MacSeg& sg, const Unit& u, uint32_t set_dw,
+                                             const uint32_t (&tv)[MAC_TAB_REGS],
+                                             uint32_t* s_tab) {
+  const uint32_t total = (sg.tab_bstride ? u.nsets : 1u) * set_dw;
+  const uint32_t* src = sg.tab + (sg.tab_bstride ? u.b_first * sg.tab_bstride : 0);
+#pragma unroll
+  for (int q = 0; q < MAC_TAB_REGS; ++q) {
+    const uint32_t t = threadIdx.x + 256u * q;
+    if (t < total) s_tab[t] = tv[q];
+  }
+  for (uint32_t t = threadIdx.x + 256u * MAC_TAB_REGS; t < total; t += 256) s_tab[t] = src[t];
+}
+
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const MacLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
+
+  // Segment of this workgroup (uniform), then its tile.
   const uint32_t wg = blockIdx.x;
   uint32_t sid = 0;
   for (uint32_t s = 1; s < L.nseg; ++s)
     if (wg >= L.seg[s].wg_begin) sid = s;
   const MacSeg& sg = L.seg[sid];
-  const uint32_t wg_local = wg - sg.wg_begin;
-  const uint32_t kpad = (sg.kin + KC - 1) / KC * KC;
+  const uint64_t tile = wg - sg.wg_begin;
+  const uint32_t kin = sg.kin, kpad = sg.kpad;
+  const uint32_t set_dw = R * kpad * 8;
 
-  stage_gf(s_gf);
-  __syncthreads();
+  const Unit u = locate(sg, tile);
+  const uint32_t* tab = s_tab + (sg.tab_bstride ? u.set * set_dw : 0u);
+  uint32_t acc[R][4];
+#pragma unroll
+  for (int i = 0; i < R; ++i)
+#pragma unroll
+    for (int w = 0; w < 4; ++w) acc[i][w] = 0;
 
-  // Contiguous tile range per workgroup: neighbouring tiles share blocks,
-  // so per-block tables are rebuilt only when the block set changes.
-  const uint64_t per = (sg.tiles + sg.wgs - 1) / sg.wgs;
-  const uint64_t t0 = (uint64_t)wg_local * per;
-  uint64_t t1 = t0 + per;
-  if (t1 > sg.tiles) t1 = sg.tiles;
-
-  if constexpr (SHARED) {
-    build_tables(sg, s_tab, lg, ex, 0, 1, R, kpad);
+  if (kin == KC) {
+    // Hot path.  The table image loads go out first (vmcnt retires in issue
+    // order, so the LDS copy then waits only for them), the KC shard loads
+    // right behind; the barrier and table copy overlap the shard loads.
+#if MEMO_EC_MAC_TABFIRST
+    uint32_t tv[MAC_TAB_REGS];
+    load_tables(sg, u, set_dw, tv);
+    uint4 d[KC];
+#pragma unroll
+    for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
+    store_tables(sg, u, set_dw, tv, s_tab);
+#else
+    uint4 d[KC];
+#pragma unroll
+    for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
+    stage_tables(sg, u, set_dw, s_tab);
+#endif
     __syncthreads();
-    for (uint64_t tile = t0; tile < t1; ++tile)
-      mac_tile<KC, R, V, true, NT>(sg, tile, s_tab, 0, kpad);
+    mac_chunk<KC, R>(acc, d, tab, kpad, 0);
   } else {
-    uint64_t have_first = ~0ull, have_last = 0;
-    for (uint64_t tile = t0; tile < t1; ++tile) {
-      uint64_t b_first, b_last;
-      if (sg.flat) {
-        const uint64_t u0 = tile * (uint64_t)(256 * V);
-        uint64_t u1 = u0 + 256 * V - 1;
-        const uint64_t total = sg.n * (uint64_t)sg.chunks;
-        if (u1 >= total) u1 = total - 1;
-        b_first = u0 / sg.chunks;
-        b_last = u1 / sg.chunks;
-      } else {
-        b_first = b_last = tile / sg.tiles_per_block;
-      }
-      if (b_first != have_first || b_last != have_last) {
-        __syncthreads();  // previous tiles' table reads are done
-        build_tables(sg, s_tab, lg, ex, b_first, (uint32_t)(b_last - b_first + 1), R, kpad);
-        __syncthreads();
-        have_first = b_first;
-        have_last = b_last;
-      }
-      mac_tile<KC, R, V, false, NT>(sg, tile, s_tab, b_first, kpad);
+    stage_tables(sg, u, set_dw, s_tab);
+    __syncthreads();
+    for (uint32_t j0 = 0; j0 < kin; j0 += KC) {
+      uint4 d[KC];
+#pragma unroll
+      for (int g = 0; g < KC; ++g)
+        if (j0 + g < kin) d[g] = ld16<NT>(u.pin + (uint64_t)(j0 + g) * sg.in_sstride);
+      mac_chunk<KC, R>(acc, d, tab, kpad, j0);
     }
+  }
+
+  if (u.valid) {
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if ((uint32_t)i < sg.r)
+        st16<NT>(u.pout + (uint64_t)i * sg.out_sstride,
+                 make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
   }
 }
 
@@ -360,11 +353,17 @@ __global__ void __launch_bounds__(256) gf_mac_kernel(const MacLaunch L) {
 // One wave per block: Gauss-Jordan on [A | I] in LDS, A = generator rows of
 // the k survivors; then rows_b[r] = C[lost[r]] * A^-1.  Lane l owns columns
 // l and l+64 of the augmented k x 2k matrix.  The field arithmetic uses the
-// LDS log/antilog image.
+// LDS log/antilog image.  Optionally emits the block's product-table image
+// (R x kpad coefficients) for gf_mac_kernel.
 __device__ __forceinline__ uint32_t gen_entry(const uint8_t* lg, const uint8_t* ex, uint32_t k,
                                               uint32_t s, uint32_t j) {
   if (s < k) return s == j ? 1u : 0u;
-  return gf_inv_lds(lg, ex, s ^ j);
+  return gf_inv_t(lg, ex, s ^ j);
+}
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
 }
 
 __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
@@ -380,10 +379,11 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
   if (b >= a.n) return;
   const uint32_t k = a.k, e = a.e, total = a.k + a.m;
   const uint32_t W = 2 * k;  // row width
-  uint8_t* M = reinterpret_cast<uint8_t*>(smem + 192) + wave * (MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K);
+  uint8_t* base = reinterpret_cast<uint8_t*>(smem + 192);
+  uint8_t* M = base + wave * (MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K);
+  uint8_t* Rw = base + 4 * (MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K) + wave * (MEMO_EC_MAX_M * MEMO_EC_MAX_K);
   const uint8_t* sidx = a.surv_idx + b * k;
   const uint8_t* lidx = a.lost_idx + b * e;
-  uint8_t* rows = a.rows + b * (uint64_t)e * k;
 
   bool bad = false;
   // [A | I]
@@ -397,14 +397,16 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
       M[r * W + col] = (uint8_t)v;
     }
   }
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  wave_sync();
 
   for (uint32_t c = 0; c < k && !bad; ++c) {
     // pivot: first row >= c with a nonzero entry in column c
     const uint32_t pv = (lane < k && lane >= c) ? M[lane * W + c] : 0u;
     const uint64_t mask = __ballot(pv != 0);
-    if (mask == 0) { bad = true; break; }
+    if (mask == 0) {
+      bad = true;
+      break;
+    }
     const uint32_t p = (uint32_t)__builtin_ctzll(mask);
     if (p != c) {
       for (uint32_t col = lane; col < W; col += 64) {
@@ -412,26 +414,22 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
         M[c * W + col] = M[p * W + col];
         M[p * W + col] = t;
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      wave_sync();
     }
-    const uint32_t iv = gf_inv_lds(lg, ex, M[c * W + c]);
+    const uint32_t iv = gf_inv_t(lg, ex, M[c * W + c]);
     __builtin_amdgcn_wave_barrier();
     for (uint32_t col = lane; col < W; col += 64)
-      M[c * W + col] = (uint8_t)gf_mul_lds(lg, ex, iv, M[c * W + col]);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      M[c * W + col] = (uint8_t)gf_mul_t(lg, ex, iv, M[c * W + col]);
+    wave_sync();
     for (uint32_t rr = 0; rr < k; ++rr) {
       if (rr == c) continue;
       const uint32_t f = M[rr * W + c];
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      wave_sync();
       if (f) {
         for (uint32_t col = lane; col < W; col += 64)
-          M[rr * W + col] ^= (uint8_t)gf_mul_lds(lg, ex, f, M[c * W + col]);
+          M[rr * W + col] ^= (uint8_t)gf_mul_t(lg, ex, f, M[c * W + col]);
       }
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      wave_sync();
     }
   }
 
@@ -443,12 +441,29 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
       uint32_t acc = 0;
       if (!lbad)
         for (uint32_t t = 0; t < k; ++t)
-          acc ^= gf_mul_lds(lg, ex, gen_entry(lg, ex, k, l, t), M[t * W + k + lane]);
-      rows[r * k + lane] = (uint8_t)acc;
+          acc ^= gf_mul_t(lg, ex, gen_entry(lg, ex, k, l, t), M[t * W + k + lane]);
+      Rw[r * k + lane] = (uint8_t)acc;
     }
     if (lbad) bad = true;
   }
-  if (bad && lane == 0 && a.status) atomicOr(a.status, 1u);
+  wave_sync();
+  if (bad) {  // invalid pattern: zero rows (zero output) + deferred error
+    for (uint32_t t = lane; t < e * k; t += 64) Rw[t] = 0;
+    wave_sync();
+    if (lane == 0 && a.status) atomicOr(a.status, 1u);
+  }
+  if (a.rows)
+    for (uint32_t t = lane; t < e * k; t += 64) a.rows[b * (uint64_t)e * k + t] = Rw[t];
+  if (a.tab) {
+    uint32_t* dst = a.tab + b * (uint64_t)a.R * a.kpad * 8;
+    const uint32_t n = a.R * a.kpad * 8;
+    for (uint32_t t = lane; t < n; t += 64) {
+      const uint32_t q = t & 7, cidx = t >> 3;
+      const uint32_t i = cidx / a.kpad, j = cidx - i * a.kpad;
+      const uint32_t c = (i < e && j < k) ? Rw[i * k + j] : 0u;
+      dst[t] = table_dword(lg, ex, c, q);
+    }
+  }
 }
 
 // ------------------------------------------------------------- synthetic fill
@@ -509,19 +524,18 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherArgs a) {
 }
 
 // ------------------------------------------------------------- launchers
-template <int KC, int R, bool SHARED>
+template <int KC, int R>
 static hipError_t launch_mac_t(const MacLaunch& L, uint32_t grid, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_V, SHARED, MAC_NT>), dim3(grid), dim3(256), lds, st,
-                     L);
+  hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
   return hipGetLastError();
 }
 
-template <int KC, bool SHARED>
+template <int KC>
 static hipError_t launch_mac_r(int R, const MacLaunch& L, uint32_t grid, size_t lds,
                                hipStream_t st) {
   switch (R) {
 #define MEMO_EC_R(x) \
-  case x: return launch_mac_t<KC, x, SHARED>(L, grid, lds, st);
+  case x: return launch_mac_t<KC, x>(L, grid, lds, st);
     MEMO_EC_R(1) MEMO_EC_R(2) MEMO_EC_R(3) MEMO_EC_R(4) MEMO_EC_R(6) MEMO_EC_R(8)
     MEMO_EC_R(12) MEMO_EC_R(16)
 #undef MEMO_EC_R
@@ -544,29 +558,23 @@ int mac_kchunk(int kin) {
   }
 }
 
-template <bool SHARED>
-static hipError_t launch_mac_k(int KC, int R, const MacLaunch& L, uint32_t grid, size_t lds,
-                               hipStream_t st) {
+hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t lds,
+                      hipStream_t st) {
   switch (KC) {
-    case 2: return launch_mac_r<2, SHARED>(R, L, grid, lds, st);
-    case 3: return launch_mac_r<3, SHARED>(R, L, grid, lds, st);
-    case 4: return launch_mac_r<4, SHARED>(R, L, grid, lds, st);
-    case 10: return launch_mac_r<10, SHARED>(R, L, grid, lds, st);
-    case 16: return launch_mac_r<16, SHARED>(R, L, grid, lds, st);
+    case 2: return launch_mac_r<2>(R, L, grid, lds, st);
+    case 3: return launch_mac_r<3>(R, L, grid, lds, st);
+    case 4: return launch_mac_r<4>(R, L, grid, lds, st);
+    case 10: return launch_mac_r<10>(R, L, grid, lds, st);
+    case 16: return launch_mac_r<16>(R, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
-}
-
-hipError_t launch_mac(int KC, int R, bool shared, const MacLaunch& L, uint32_t grid, size_t lds,
-                      hipStream_t st) {
-  return shared ? launch_mac_k<true>(KC, R, L, grid, lds, st)
-                : launch_mac_k<false>(KC, R, L, grid, lds, st);
 }
 
 hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st) {
   const uint32_t grid = (uint32_t)((a.n + 3) / 4);
   if (grid == 0) return hipSuccess;
-  const size_t lds = 768 + 4 * (size_t)MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K;
+  const size_t lds = 768 + 4 * (size_t)MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K +
+                     4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
   hipLaunchKernelGGL(decode_rows_kernel, dim3(grid), dim3(256), lds, st, a);
   return hipGetLastError();
 }

@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -25,15 +26,19 @@ struct memo_ec_ctx {
   hipStream_t stream = nullptr;   // stream MEMO_EC_DEVICE work goes to
   hipStream_t aux[2] = {nullptr, nullptr};  // host-pipeline streams
   uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
-  uint8_t* d_rows = nullptr;      // decode rows scratch
-  size_t rows_cap = 0;
+  uint32_t* d_tabs = nullptr;     // per-block product-table images (rebuild)
+  size_t tabs_cap = 0;            // bytes
+  struct TabEntry {
+    int k, m, R, kpad;
+    uint32_t* dev;
+  };
+  std::vector<TabEntry> enc_tabs;  // cached encode images per (k, m, R, kpad)
   // host pipeline: device slots and pinned bounce buffers
   uint8_t* d_slot[2] = {nullptr, nullptr};
   size_t slot_cap = 0;
   uint8_t* h_slot[2] = {nullptr, nullptr};
   size_t hslot_cap = 0;
   int deferred = 0;
-  int cus = 256;
 };
 
 namespace {
@@ -75,102 +80,108 @@ int check_km(int k, int m) {
 struct Plan {
   MacSeg seg{};
   int KC = 4, R = 1;
-  size_t lds = 0;  // table bytes (without the 768-byte GF image)
-  bool shared = true;
+  size_t lds = 0;  // LDS bytes of this segment's table sets
 };
+
+uint32_t kpad_of(uint32_t kin, int KC) { return (kin + KC - 1) / KC * KC; }
+
+// Blocks a 256-column tile can touch (flat mapping).
+uint64_t sets_per_tile(uint64_t C) { return (MAC_TILE - 1 + C - 1) / C + 1; }
 
 Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* in,
                   uint64_t in_bs, uint64_t in_ss, uint8_t* out, uint64_t out_bs, uint64_t out_ss,
-                  const uint8_t* coef, uint64_t coef_bs, int KC, int R) {
+                  const uint32_t* tab, uint64_t tab_bs_dw, int KC, int R) {
   Plan p;
   p.KC = KC;
   p.R = R;
-  p.shared = coef_bs == 0;
   MacSeg& s = p.seg;
-  s.in = in; s.out = out; s.coef = coef;
+  s.in = in; s.out = out; s.tab = tab;
   s.in_bstride = in_bs; s.in_sstride = in_ss;
   s.out_bstride = out_bs; s.out_sstride = out_ss;
-  s.coef_bstride = coef_bs;
+  s.tab_bstride = tab_bs_dw;
   s.n = n; s.kin = kin; s.r = r;
+  s.kpad = kpad_of(kin, KC);
   s.chunks = (uint32_t)(S / 16);
-  const uint32_t kpad = (kin + KC - 1) / KC * KC;
-  const size_t set_bytes = (size_t)R * kpad * 32;
+  const size_t set_bytes = (size_t)R * s.kpad * 32;
   const uint64_t C = s.chunks;
-  if (p.shared) {
+  if (tab_bs_dw == 0) {  // one image for every block
     s.flat = 1;
     p.lds = set_bytes;
+  } else if (sets_per_tile(C) * set_bytes <= kLdsBudget) {
+    s.flat = 1;
+    p.lds = sets_per_tile(C) * set_bytes;
   } else {
-    const uint64_t nsets = (MAC_UNITS + C - 1) / C + 1;
-    if (nsets * set_bytes <= kLdsBudget) {
-      s.flat = 1;
-      p.lds = nsets * set_bytes;
-    } else {
-      s.flat = 0;
-      p.lds = set_bytes;
-    }
+    s.flat = 0;
+    p.lds = set_bytes;
   }
   if (s.flat) {
-    s.tiles = (n * C + MAC_UNITS - 1) / MAC_UNITS;
+    s.tiles = (n * C + MAC_TILE - 1) / MAC_TILE;
     s.tiles_per_block = 0;
   } else {
-    s.tiles_per_block = (C + MAC_UNITS - 1) / MAC_UNITS;
+    s.tiles_per_block = (C + MAC_TILE - 1) / MAC_TILE;
     s.tiles = n * s.tiles_per_block;
   }
   return p;
 }
 
-// Launch 1..MEMO_EC_MAX_SEGMENTS planned segments as one kernel.  All must
-// share `shared`; KC/R are unified to the common bound.
-int launch_plans(memo_ec_ctx* ctx, std::vector<Plan>& plans, hipStream_t st) {
+// Launch 1..MEMO_EC_MAX_SEGMENTS planned segments as one kernel, one tile
+// per workgroup.  All share KC and R (the common compile-time bounds).
+int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   if (plans.empty()) return MEMO_EC_OK;
   MacLaunch L{};
   L.nseg = 0;
-  uint64_t total_tiles = 0;
+  uint64_t wg = 0;
   size_t lds = 0;
-  int KC = plans[0].KC, R = 0;
-  const bool shared = plans[0].shared;
+  const int KC = plans[0].KC, R = plans[0].R;
   for (auto& p : plans) {
-    if (p.KC != KC) return MEMO_EC_EINVAL;
-    if (p.shared != shared) return MEMO_EC_EINVAL;
-    R = std::max(R, p.R);
-    total_tiles += p.seg.tiles;
-  }
-  if (total_tiles == 0) return MEMO_EC_OK;
-  // Workgroup budget: enough waves to keep every CU streaming, each
-  // workgroup walking a contiguous range of tiles.
-  const uint64_t cap = (uint64_t)ctx->cus * 8;
-  const uint64_t want = std::min<uint64_t>(total_tiles, cap);
-  uint32_t wg = 0;
-  for (auto& p : plans) {
+    if (p.KC != KC || p.R != R) return MEMO_EC_EINVAL;
     if (p.seg.tiles == 0) continue;
-    uint64_t w = (want * p.seg.tiles + total_tiles - 1) / total_tiles;
-    w = std::max<uint64_t>(1, std::min<uint64_t>(w, p.seg.tiles));
-    p.seg.wg_begin = wg;
-    p.seg.wgs = (uint32_t)w;
-    wg += (uint32_t)w;
-    // recompute LDS with the unified R
-    const uint32_t kpad = (p.seg.kin + KC - 1) / KC * KC;
-    const size_t set_bytes = (size_t)R * kpad * 32;
-    size_t need = set_bytes;
-    if (!shared && p.seg.flat) need = ((MAC_UNITS + p.seg.chunks - 1) / p.seg.chunks + 1) * set_bytes;
-    lds = std::max(lds, need);
+    p.seg.wg_begin = (uint32_t)wg;
+    wg += p.seg.tiles;
+    lds = std::max(lds, p.lds);
     L.seg[L.nseg++] = p.seg;
   }
-  if (lds + 768 > 160 * 1024) return MEMO_EC_ERANGE;
-  hipError_t e = launch_mac(KC, R, shared, L, wg, 768 + lds, st);
-  return hip_rc(e);
+  if (wg == 0) return MEMO_EC_OK;
+  if (wg > 0x7fffffffull) return MEMO_EC_ERANGE;
+  if (lds > 160 * 1024) return MEMO_EC_ERANGE;
+  return hip_rc(launch_mac(KC, R, L, (uint32_t)wg, lds, st));
 }
 
-int ensure_rows(memo_ec_ctx* ctx, size_t bytes) {
-  if (bytes <= ctx->rows_cap) return MEMO_EC_OK;
-  if (ctx->d_rows) {
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    HIPCHK(hipFree(ctx->d_rows));
-    ctx->d_rows = nullptr;
+// Cached device table image of the Cauchy parity rows of (k, m).
+int encode_tables(memo_ec_ctx* ctx, int k, int m, int R, int KC, const uint32_t** out) {
+  const int kpad = (int)kpad_of((uint32_t)k, KC);
+  for (auto& e : ctx->enc_tabs)
+    if (e.k == k && e.m == m && e.R == R && e.kpad == kpad) {
+      *out = e.dev;
+      return MEMO_EC_OK;
+    }
+  std::vector<uint8_t> gen((size_t)(k + m) * k);
+  if (int rc = memo_ec_generator(k, m, gen.data())) return rc;
+  std::vector<uint32_t> img((size_t)R * kpad * 8);
+  table_image_host(gen.data() + (size_t)k * k, (uint32_t)m, (uint32_t)k, (uint32_t)R,
+                   (uint32_t)kpad, img.data());
+  uint32_t* dev = nullptr;
+  HIPCHK(hipMalloc(&dev, img.size() * 4));
+  hipError_t e = hipMemcpy(dev, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(dev);
+    return hip_rc(e);
   }
-  size_t cap = std::max<size_t>(bytes, 1 << 20);
-  HIPCHK(hipMalloc(&ctx->d_rows, cap));
-  ctx->rows_cap = cap;
+  ctx->enc_tabs.push_back({k, m, R, kpad, dev});
+  *out = dev;
+  return MEMO_EC_OK;
+}
+
+int ensure_tabs(memo_ec_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->tabs_cap) return MEMO_EC_OK;
+  if (ctx->d_tabs) {
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipFree(ctx->d_tabs));
+    ctx->d_tabs = nullptr;
+  }
+  const size_t cap = std::max<size_t>(bytes, 1 << 20);
+  HIPCHK(hipMalloc(&ctx->d_tabs, cap));
+  ctx->tabs_cap = cap;
   return MEMO_EC_OK;
 }
 
@@ -196,25 +207,56 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
   return MEMO_EC_OK;
 }
 
+// Largest batch (blocks) one MAC launch takes: tiles must fit a 31-bit grid.
+size_t max_blocks_per_launch(size_t S) {
+  const uint64_t per = (S / 16 + MAC_TILE - 1) / MAC_TILE + 1;
+  return (size_t)std::max<uint64_t>(1, (0x7fffffffull - MAC_TILE) / per);
+}
+
 // Device-resident encode on stream st.
 int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* data,
                   uint8_t* parity, hipStream_t st) {
-  std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)m, S, n, data, (uint64_t)k * S, S,
-                                       parity, (uint64_t)m * S, S, nullptr, 0, mac_kchunk(k),
-                                       mac_rbound(m))};
-  return launch_plans(ctx, plans, st);
+  const int KC = mac_kchunk(k), R = mac_rbound(m);
+  const uint32_t* tab = nullptr;
+  if (int rc = encode_tables(ctx, k, m, R, KC, &tab)) return rc;
+  const size_t step = max_blocks_per_launch(S);
+  for (size_t b0 = 0; b0 < n; b0 += step) {
+    const size_t cnt = std::min(step, n - b0);
+    std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)m, S, cnt,
+                                         data + b0 * (size_t)k * S, (uint64_t)k * S, S,
+                                         parity + b0 * (size_t)m * S, (uint64_t)m * S, S, tab, 0,
+                                         KC, R)};
+    if (int rc = launch_plans(plans, st)) return rc;
+  }
+  return MEMO_EC_OK;
 }
 
-// Device-resident rebuild on stream st: decode rows then the MAC.
+// Device-resident rebuild on stream st: decode rows (+ per-block table
+// images) then the MAC.  `rows` may be null; `tabs` has room for n images.
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
-                   uint8_t* rows, hipStream_t st) {
-  DecodeArgs a{surv_idx, lost_idx, rows, ctx->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e};
+                   uint8_t* rows, uint32_t* tabs, hipStream_t st) {
+  const int KC = mac_kchunk(k), R = mac_rbound(e);
+  const uint32_t kpad = kpad_of((uint32_t)k, KC);
+  const uint64_t img_dw = (uint64_t)R * kpad * 8;
+  DecodeArgs a{surv_idx, lost_idx, rows, tabs, ctx->d_status, n, (uint32_t)k, (uint32_t)m,
+               (uint32_t)e, (uint32_t)R, kpad};
   HIPCHK(launch_decode_rows(a, st));
-  std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, n, surv, (uint64_t)k * S, S,
-                                       out, (uint64_t)e * S, S, rows, (uint64_t)e * k,
-                                       mac_kchunk(k), mac_rbound(e))};
-  return launch_plans(ctx, plans, st);
+  const size_t step = max_blocks_per_launch(S);
+  for (size_t b0 = 0; b0 < n; b0 += step) {
+    const size_t cnt = std::min(step, n - b0);
+    std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, cnt,
+                                         surv + b0 * (size_t)k * S, (uint64_t)k * S, S,
+                                         out + b0 * (size_t)e * S, (uint64_t)e * S, S,
+                                         tabs + b0 * img_dw, img_dw, KC, R)};
+    if (int rc = launch_plans(plans, st)) return rc;
+  }
+  return MEMO_EC_OK;
+}
+
+size_t tab_bytes(int k, int e, size_t n) {
+  const int KC = mac_kchunk(k), R = mac_rbound(e);
+  return n * (size_t)R * kpad_of((uint32_t)k, KC) * 32;
 }
 
 int take_deferred(memo_ec_ctx* ctx) {
@@ -278,9 +320,6 @@ int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
   auto* c = new (std::nothrow) memo_ec_ctx;
   if (!c) return MEMO_EC_ENOMEM;
   c->device = device;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
-    c->cus = prop.multiProcessorCount;
   int rc = MEMO_EC_OK;
   if ((rc = hip_rc(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking))) ||
       (rc = hip_rc(hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking))) ||
@@ -306,7 +345,8 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
     if (p) (void)hipFree(p);
   for (auto& p : c->h_slot)
     if (p) (void)hipHostFree(p);
-  if (c->d_rows) (void)hipFree(c->d_rows);
+  if (c->d_tabs) (void)hipFree(c->d_tabs);
+  for (auto& e : c->enc_tabs) (void)hipFree(e.dev);
   if (c->d_status) (void)hipFree(c->d_status);
   for (auto& st : c->aux)
     if (st) (void)hipStreamDestroy(st);
@@ -389,7 +429,8 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   if (n == 0 || e == 0) return MEMO_EC_OK;
   if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
-  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e};
+  DecodeArgs a{surv_idx, lost_idx, rows, nullptr, c->d_status, n, (uint32_t)k, (uint32_t)m,
+               (uint32_t)e, 0, 0};
   return hip_rc(launch_decode_rows(a, c->stream));
 }
 
@@ -403,8 +444,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
   if (where == MEMO_EC_DEVICE) {
-    if (int rc = ensure_rows(c, n * (size_t)e * k)) return rc;
-    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_rows, c->stream);
+    if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
+    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, nullptr, c->d_tabs,
+                          c->stream);
   }
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
@@ -416,7 +458,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   // slot layout: [surv | out | surv_idx | lost_idx], host bounce likewise
   const size_t slot = nb * (in_b + out_b + idx_b);
   if (int rc = ensure_slots(c, slot, slot)) return rc;
-  if (int rc = ensure_rows(c, 2 * nb * (size_t)e * k)) return rc;
+  if (int rc = ensure_tabs(c, 2 * tab_bytes(k, e, nb))) return rc;
   const size_t nbatch = (n + nb - 1) / nb;
   std::vector<size_t> pend_off(2, 0), pend_cnt(2, 0);
   auto drain = [&](int s) -> int {
@@ -448,8 +490,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       src = h;
     }
     HIPCHK(hipMemcpyAsync(dsurv, src, cnt * in_b, hipMemcpyHostToDevice, c->aux[s]));
-    uint8_t* rows = c->d_rows + (size_t)s * nb * e * k;
-    if (int rc = rebuild_device(c, k, m, S, cnt, dsidx, dsurv, dlidx, e, dout, rows, c->aux[s]))
+    uint32_t* tabs = c->d_tabs + (size_t)s * tab_bytes(k, e, nb) / 4;
+    if (int rc = rebuild_device(c, k, m, S, cnt, dsidx, dsurv, dlidx, e, dout, nullptr, tabs,
+                                c->aux[s]))
       return rc;
     uint8_t* dst = pinned ? out + b0 * out_b : h + cnt * in_b;
     HIPCHK(hipMemcpyAsync(dst, dout, cnt * out_b, hipMemcpyDeviceToHost, c->aux[s]));
@@ -463,29 +506,32 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
 
 int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* segs) {
   if (!c || nseg < 0 || nseg > MEMO_EC_MAX_SEGMENTS || (nseg && !segs)) return MEMO_EC_EINVAL;
-  // common chunk: the specialised k when all segments share it, else 4
-  int KC = -1;
+  // common bounds: the specialised chunk when every segment has the same k,
+  // else 4; R = the largest m's bound (smaller m's rows are zero tables)
+  int KC = -1, R = 1;
   for (int i = 0; i < nseg; ++i) {
     if (int rc = check_km(segs[i].k, segs[i].m)) return rc;
     if (segs[i].m == 0 || segs[i].n == 0) continue;
     if (segs[i].S == 0 || segs[i].S % 64 || !segs[i].data || !segs[i].parity)
       return MEMO_EC_EINVAL;
+    if (segs[i].n > max_blocks_per_launch(segs[i].S)) return MEMO_EC_ERANGE;
     const int kc = mac_kchunk(segs[i].k);
     KC = (KC < 0 || KC == kc) ? kc : 4;
+    R = std::max(R, mac_rbound(segs[i].m));
   }
   if (KC < 0) return MEMO_EC_OK;
-  int R = 1;
-  for (int i = 0; i < nseg; ++i) R = std::max(R, mac_rbound(segs[i].m));
   DeviceGuard g(c->device);
   std::vector<Plan> plans;
   for (int i = 0; i < nseg; ++i) {
     const auto& s = segs[i];
     if (s.m == 0 || s.n == 0) continue;
+    const uint32_t* tab = nullptr;
+    if (int rc = encode_tables(c, s.k, s.m, R, KC, &tab)) return rc;
     plans.push_back(plan_segment((uint32_t)s.k, (uint32_t)s.m, s.S, s.n, s.data,
                                  (uint64_t)s.k * s.S, s.S, s.parity, (uint64_t)s.m * s.S, s.S,
-                                 nullptr, 0, KC, R));
+                                 tab, 0, KC, R));
   }
-  return launch_plans(c, plans, c->stream);
+  return launch_plans(plans, c->stream);
 }
 
 int memo_ec_fill_blocks(memo_ec_ctx* c, uint64_t seed, uint64_t first_block, size_t n, size_t B,
