@@ -104,6 +104,54 @@ static float time_ms(F f, int iters) {
   return ts[ts.size() / 2];
 }
 
+
+// Generalised shard pattern: WG threads T, each lane W consecutive uint4 of
+// one shard column (W=1: 16 B, W=2: 32 B), ORDER 0 = tiles of one block are
+// consecutive workgroups, 1 = consecutive workgroups walk different blocks.
+template <int K, int R, int T, int W, int ORDER>
+__global__ void __launch_bounds__(T) k_shards2(const uint8_t* in, uint8_t* out, size_t n,
+                                               uint32_t C, size_t S) {
+  const uint32_t cols_per_wg = T * W;
+  const uint32_t tpb = (C + cols_per_wg - 1) / cols_per_wg;
+  size_t b, t;
+  if (ORDER == 0) { b = blockIdx.x / tpb; t = blockIdx.x % tpb; }
+  else { b = blockIdx.x % n; t = blockIdx.x / n; }
+  if (b >= n) return;
+  const uint32_t c0 = t * cols_per_wg + threadIdx.x * W;
+  if (c0 >= C) return;
+  const uint8_t* p = in + b * K * S + (size_t)c0 * 16;
+  u32x4 d[K][W];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      d[j][w] = (c0 + w < C) ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + j * S) + w)
+                             : u32x4{0, 0, 0, 0};
+  uint8_t* o = out + b * R * S + (size_t)c0 * 16;
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    u32x4 a = d[0][w];
+#pragma unroll
+    for (int j = 1; j < K; ++j) a ^= d[j][w];
+    if (c0 + w < C)
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        u32x4 v = a;
+        v.x += i;
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + i * S) + w);
+      }
+  }
+}
+
+template <int T, int W, int ORDER>
+static void run2(const uint8_t* din, uint8_t* dout, size_t n, uint32_t C, size_t S, double alg) {
+  const uint32_t tpb = (C + T * W - 1) / (T * W);
+  const int grid = (int)(tpb * n);
+  float t = time_ms([&] { k_shards2<10, 4, T, W, ORDER><<<grid, T>>>(din, dout, n, C, S); }, 10);
+  printf("{\"probe\":\"shards2\",\"S\":%zu,\"T\":%d,\"W\":%d,\"order\":%d,\"ms\":%.4f,\"TBs\":%.3f}\n", S, T, W,
+         ORDER, t, alg / t / 1e9);
+}
+
 int main() {
   const size_t bytes = 4ull << 30;  // 4 GiB each side
   uint8_t *in, *out;
@@ -113,7 +161,7 @@ int main() {
   CHK(hipMemset(out, 0, bytes));
   const size_t n4 = bytes / 16;
   const int iters = 10;
-  for (int grid : {2048, 8192, 65536}) {
+  for (int grid : {65536}) {
     float t;
     t = time_ms([&] { k_copy<false><<<grid, 256>>>((u32x4*)in, (u32x4*)out, n4); }, iters);
     printf("{\"probe\":\"copy\",\"nt\":0,\"grid\":%d,\"ms\":%.4f,\"TBs\":%.3f}\n", grid, t, 2.0 * bytes / t / 1e9);
@@ -133,7 +181,7 @@ int main() {
     CHK(hipMemset(din, 3, n * 10 * S));
     const uint32_t C = S / 16;
     const double alg = (double)n * 14 * S;
-    for (int pt : {1, 2, 4, 8}) {
+    for (int pt : {1}) {
       const size_t total = n * C;
       const int grid = (int)((total + 256 * pt - 1) / (256 * pt));
       float t0 = time_ms([&] { k_shards<10, 4, false><<<grid, 256>>>(din, dout, n, C, S, pt); }, iters);
@@ -141,6 +189,16 @@ int main() {
       printf("{\"probe\":\"shards10x4\",\"S\":%zu,\"per_thread\":%d,\"ms_plain\":%.4f,\"TBs_plain\":%.3f,\"ms_nt\":%.4f,\"TBs_nt\":%.3f}\n",
              S, pt, t0, alg / t0 / 1e9, t1, alg / t1 / 1e9);
     }
+    run2<64, 1, 0>(din, dout, n, C, S, alg);
+    run2<128, 1, 0>(din, dout, n, C, S, alg);
+    run2<256, 1, 0>(din, dout, n, C, S, alg);
+    run2<512, 1, 0>(din, dout, n, C, S, alg);
+    run2<1024, 1, 0>(din, dout, n, C, S, alg);
+    run2<256, 1, 1>(din, dout, n, C, S, alg);
+    run2<512, 1, 1>(din, dout, n, C, S, alg);
+    run2<256, 2, 0>(din, dout, n, C, S, alg);
+    run2<128, 2, 0>(din, dout, n, C, S, alg);
+    run2<256, 2, 1>(din, dout, n, C, S, alg);
     CHK(hipFree(din));
     CHK(hipFree(dout));
   }
