@@ -1,0 +1,661 @@
+// erasure_consensus.cc -- see erasure_consensus.hh.
+#include "erasure_consensus.hh"
+
+#include <nmmintrin.h>
+
+#include <algorithm>
+#include <chrono>
+#include <set>
+
+namespace memo_host {
+
+namespace {
+// Batches mix shard sizes within a power-of-two bucket: every byte column is
+// coded independently, so a shard zero-padded to the batch's largest S codes
+// exactly (the tail codes to zero and is dropped); padding stays below 2x.
+int size_bucket(size_t S) {
+  int b = 0;
+  while (S > 64) {
+    S >>= 1;
+    ++b;
+  }
+  return b;
+}
+
+void check(int rc, const char* what) {
+  if (rc != MEMO_EC_OK) throw Error(std::string("memo_ec ") + what + ": " + memo_ec_strerror(rc));
+}
+}  // namespace
+
+// ------------------------------------------------------------------ codec
+Codec::Codec(int device, int contexts) {
+  for (int i = 0; i < contexts; ++i) {
+    memo_ec_ctx* c = nullptr;
+    const int rc = memo_ec_ctx_create(device, &c);
+    if (rc != MEMO_EC_OK) {
+      for (auto* p : all_) memo_ec_ctx_destroy(p);
+      throw Error(std::string("memo_ec ctx_create: ") + memo_ec_strerror(rc));
+    }
+    all_.push_back(c);
+    free_.push_back(c);
+  }
+}
+
+Codec::~Codec() {
+  for (auto* c : all_) memo_ec_ctx_destroy(c);
+}
+
+memo_ec_ctx* Codec::acquire() {
+  std::unique_lock<std::mutex> l(mu_);
+  cv_.wait(l, [&] { return !free_.empty(); });
+  auto* c = free_.back();
+  free_.pop_back();
+  return c;
+}
+
+void Codec::release(memo_ec_ctx* c) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back(c);
+  }
+  cv_.notify_one();
+}
+
+void Codec::encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity) {
+  auto* c = acquire();
+  const int rc = memo_ec_encode_batch(c, k, m, S, n, data, parity, MEMO_EC_HOST);
+  release(c);
+  ++encode_calls_;
+  check(rc, "encode");
+}
+
+void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
+                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out) {
+  auto* c = acquire();
+  const int rc = memo_ec_rebuild_batch(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, MEMO_EC_HOST);
+  release(c);
+  ++rebuild_calls_;
+  check(rc, "rebuild");
+}
+
+// ---------------------------------------------------------- shard format
+uint32_t crc32c(const uint8_t* p, size_t n) {
+  uint64_t c = 0xFFFFFFFFu;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t v;
+    std::memcpy(&v, p + i, 8);
+    c = _mm_crc32_u64(c, v);
+  }
+  uint32_t c32 = (uint32_t)c;
+  for (; i < n; ++i) c32 = _mm_crc32_u8(c32, p[i]);
+  return c32 ^ 0xFFFFFFFFu;
+}
+
+Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
+  if (h.salt.size() > 32) throw Error("shard: salt longer than 32 bytes");
+  Buffer w(ShardHeader::kSize + h.shard_size, 0);
+  std::memcpy(w.data(), "MECS", 4);
+  w[4] = h.version;
+  w[5] = h.k;
+  w[6] = h.m;
+  w[7] = h.index;
+  std::memcpy(w.data() + 8, &h.block_size, 8);
+  std::memcpy(w.data() + 16, &h.shard_size, 8);
+  std::memcpy(w.data() + 24, h.address.value.data(), 32);
+  const uint32_t sl = (uint32_t)h.salt.size();
+  std::memcpy(w.data() + 56, &sl, 4);
+  if (sl) std::memcpy(w.data() + 60, h.salt.data(), sl);
+  const uint32_t crc = crc32c(payload, h.shard_size);
+  std::memcpy(w.data() + 92, &crc, 4);
+  std::memcpy(w.data() + ShardHeader::kSize, payload, h.shard_size);
+  return w;
+}
+
+ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
+  if (w.size() < ShardHeader::kSize || std::memcmp(w.data(), "MECS", 4) != 0)
+    throw ValidationFailed("shard: bad magic");
+  ShardHeader h;
+  h.version = w[4];
+  h.k = w[5];
+  h.m = w[6];
+  h.index = w[7];
+  std::memcpy(&h.block_size, w.data() + 8, 8);
+  std::memcpy(&h.shard_size, w.data() + 16, 8);
+  h.address = Address(w.data() + 24, 0, false);
+  uint32_t sl;
+  std::memcpy(&sl, w.data() + 56, 4);
+  if (sl > 32) throw ValidationFailed("shard: bad salt length");
+  h.salt.assign(w.begin() + 60, w.begin() + 60 + sl);
+  std::memcpy(&h.crc, w.data() + 92, 4);
+  if (h.version != 1) throw ValidationFailed("shard: unknown version");
+  if (h.k < 1 || h.index >= h.k + h.m) throw ValidationFailed("shard: bad geometry");
+  if (h.shard_size != memo_ec_shard_size(h.block_size, h.k))
+    throw ValidationFailed("shard: size does not match block size");
+  if (w.size() != ShardHeader::kSize + h.shard_size) throw ValidationFailed("shard: truncated");
+  if (crc32c(w.data() + ShardHeader::kSize, h.shard_size) != h.crc)
+    throw ValidationFailed("shard: checksum mismatch");
+  if (payload) *payload = w.data() + ShardHeader::kSize;
+  return h;
+}
+
+Key shard_key(const Address& a, int index) {
+  uint8_t tag[16] = {'m', 'e', 'm', 'o', '-', 'e', 'c', '-', 's', 'h', 'a', 'r', 'd', 0, 0, 0};
+  tag[15] = (uint8_t)index;
+  const auto h = sha256(a.value.data(), 32, tag, sizeof tag);
+  return Address(h.data(), flags::immutable_block, true);
+}
+
+// ------------------------------------------------------------ thread pool
+ThreadPool::ThreadPool(int n) {
+  for (int i = 0; i < std::max(1, n); ++i) ts_.emplace_back([this] { worker(); });
+}
+
+ThreadPool::~ThreadPool() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : ts_) t.join();
+}
+
+void ThreadPool::worker() {
+  for (;;) {
+    std::function<void()> f;
+    {
+      std::unique_lock<std::mutex> l(mu_);
+      cv_.wait(l, [&] { return stop_ || !q_.empty(); });
+      if (stop_ && q_.empty()) return;
+      f = std::move(q_.front());
+      q_.pop_front();
+    }
+    f();
+  }
+}
+
+void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
+  if (n == 0) return;
+  std::mutex dm;
+  std::condition_variable dcv;
+  size_t done = 0;
+  std::exception_ptr err;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (size_t i = 0; i < n; ++i)
+      q_.push_back([&, i] {
+        try {
+          fn(i);
+        } catch (...) {
+          std::lock_guard<std::mutex> g2(dm);
+          if (!err) err = std::current_exception();
+        }
+        std::lock_guard<std::mutex> g2(dm);
+        if (++done == n) dcv.notify_all();
+      });
+  }
+  cv_.notify_all();
+  std::unique_lock<std::mutex> l(dm);
+  dcv.wait(l, [&] { return done == n; });
+  if (err) std::rethrow_exception(err);
+}
+
+// --------------------------------------------------------------- plugin
+ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& overlay,
+                                   ErasureOptions o)
+    : StackedConsensus(std::move(backend)),
+      overlay_(overlay),
+      o_(o),
+      codec_(o.device, 4),
+      pool_(o.threads) {
+  if (o_.k < 1 || o_.m < 1 || o_.k > MEMO_EC_MAX_K || o_.m > MEMO_EC_MAX_M)
+    throw Error("erasure: bad (k, m)");
+  bthread_ = std::thread([this] { batcher_loop(); });
+}
+
+ErasureConsensus::~ErasureConsensus() {
+  {
+    std::lock_guard<std::mutex> g(bmu_);
+    bstop_ = true;
+  }
+  bcv_.notify_all();
+  bthread_.join();
+}
+
+std::string ErasureConsensus::redundancy() const {
+  char f[32];
+  std::snprintf(f, sizeof f, "%.4g", double(o_.k + o_.m) / o_.k);
+  return to_json({{"type", "erasure"},
+                  {"k", std::to_string(o_.k)},
+                  {"m", std::to_string(o_.m)},
+                  {"desired_factor", f}});
+}
+
+std::string ErasureConsensus::stats() const {
+  size_t blocks;
+  {
+    std::lock_guard<std::mutex> g(index_mu_);
+    blocks = index_.size();
+  }
+  return to_json({{"blocks", std::to_string(blocks)},
+                  {"stored", std::to_string(stored_)},
+                  {"fetched", std::to_string(fetched_)},
+                  {"decoded", std::to_string(decoded_)},
+                  {"repaired", std::to_string(repaired_)},
+                  {"encode_calls", std::to_string(codec_.encode_calls())},
+                  {"rebuild_calls", std::to_string(codec_.rebuild_calls())}});
+}
+
+Buffer ErasureConsensus::padded(const Block& b, size_t S) const {
+  Buffer p((size_t)o_.k * S, 0);
+  std::copy(b.data.begin(), b.data.end(), p.begin());
+  return p;
+}
+
+// The batcher thread: gathers concurrent store() calls (up to batch_max
+// blocks or batch_window_us) and encodes each same-shard-size group with one
+// GPU call -- the GPU needs many blocks per launch to stream at HBM speed.
+void ErasureConsensus::batcher_loop() {
+  for (;;) {
+    std::vector<EncodeJob*> jobs;
+    {
+      std::unique_lock<std::mutex> l(bmu_);
+      bcv_.wait(l, [&] { return bstop_ || !bq_.empty(); });
+      if (bstop_ && bq_.empty()) return;
+      const auto deadline =
+          std::chrono::steady_clock::now() + std::chrono::microseconds(o_.batch_window_us);
+      while ((int)bq_.size() < o_.batch_max && !bstop_ &&
+             bcv_.wait_until(l, deadline) != std::cv_status::timeout) {
+      }
+      while (!bq_.empty() && (int)jobs.size() < o_.batch_max) {
+        jobs.push_back(bq_.front());
+        bq_.pop_front();
+      }
+    }
+    std::map<int, std::vector<EncodeJob*>> by_s;
+    for (auto* j : jobs) by_s[size_bucket(memo_ec_shard_size(j->block->data.size(), o_.k))].push_back(j);
+    for (auto& g : by_s) {
+      const size_t n = g.second.size();
+      size_t S = 0;
+      for (auto* j : g.second) S = std::max(S, memo_ec_shard_size(j->block->data.size(), o_.k));
+      try {
+        Buffer data(n * o_.k * S, 0), parity(n * o_.m * S);
+        for (size_t i = 0; i < n; ++i) {
+          const auto& d = g.second[i]->block->data;
+          const size_t Sb = memo_ec_shard_size(d.size(), o_.k);
+          for (int j = 0; j < o_.k; ++j) {
+            const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
+            std::copy(d.begin() + lo, d.begin() + hi, data.begin() + (i * o_.k + j) * S);
+          }
+        }
+        codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
+        for (size_t i = 0; i < n; ++i) {
+          const size_t Sb = memo_ec_shard_size(g.second[i]->block->data.size(), o_.k);
+          Buffer p((size_t)o_.m * Sb);
+          for (int r = 0; r < o_.m; ++r)
+            std::copy(parity.begin() + (i * o_.m + r) * S, parity.begin() + (i * o_.m + r) * S + Sb,
+                      p.begin() + (size_t)r * Sb);
+          g.second[i]->parity.set_value(std::move(p));
+        }
+      } catch (...) {
+        for (auto* j : g.second) j->parity.set_exception(std::current_exception());
+      }
+    }
+  }
+}
+
+// Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360).
+void ErasureConsensus::place(const Block& b, const Buffer& parity) {
+  const int total = o_.k + o_.m;
+  const size_t S = memo_ec_shard_size(b.data.size(), o_.k);
+  const Buffer data = padded(b, S);
+  auto owners = overlay_.allocate(b.address, total);
+  if ((int)owners.size() < o_.k)
+    throw TooFewPeers("erasure: " + std::to_string(owners.size()) + " reachable owners, need " +
+                      std::to_string(o_.k));
+  Placement pl;
+  pl.B = b.data.size();
+  pl.salt = b.salt;
+  pl.owner.assign(total, Address());
+  std::vector<int> ok(total, 0);
+  pool_.parallel_for(owners.size(), [&](size_t i) {
+    ShardHeader h;
+    h.k = (uint8_t)o_.k;
+    h.m = (uint8_t)o_.m;
+    h.index = (uint8_t)i;
+    h.block_size = b.data.size();
+    h.shard_size = S;
+    h.address = b.address;
+    h.salt = b.salt;
+    const uint8_t* p = i < (size_t)o_.k ? data.data() + i * S : parity.data() + (i - o_.k) * S;
+    try {
+      owners[i]->store(shard_key(b.address, (int)i), encode_shard(h, p));
+      ok[i] = 1;
+    } catch (Unavailable&) {
+    }
+  });
+  int reached = 0;
+  for (size_t i = 0; i < owners.size(); ++i)
+    if (ok[i]) {
+      pl.owner[i] = owners[i]->id;
+      ++reached;
+    }
+  {
+    std::lock_guard<std::mutex> g(index_mu_);
+    index_[b.address] = pl;
+  }
+  if (reached < o_.k)
+    throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
+                      std::to_string(o_.k));
+  ++stored_;
+}
+
+void ErasureConsensus::_store(const Block& b, StoreMode mode) {
+  if (b.is_mutable || b.address.mutable_block()) return backend_->store(b, mode);
+  if (!chb_valid(b.address, b.salt, b.data)) throw ValidationFailed("CHB address mismatch");
+  EncodeJob job{&b, {}};
+  auto fut = job.parity.get_future();
+  {
+    std::lock_guard<std::mutex> g(bmu_);
+    bq_.push_back(&job);
+  }
+  bcv_.notify_all();
+  place(b, fut.get());
+}
+
+void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
+  std::vector<const Block*> imm;
+  for (auto& b : blocks) {
+    if (b.is_mutable || b.address.mutable_block()) backend_->store(b, STORE_INSERT);
+    else imm.push_back(&b);
+  }
+  for (size_t b0 = 0; b0 < imm.size(); b0 += o_.batch_max) {
+    const size_t n0 = std::min<size_t>(o_.batch_max, imm.size() - b0);
+    std::map<int, std::vector<const Block*>> by_s;
+    for (size_t i = 0; i < n0; ++i) {
+      const Block* b = imm[b0 + i];
+      if (!chb_valid(b->address, b->salt, b->data)) throw ValidationFailed("CHB address mismatch");
+      by_s[size_bucket(memo_ec_shard_size(b->data.size(), o_.k))].push_back(b);
+    }
+    for (auto& g : by_s) {
+      const size_t n = g.second.size();
+      size_t S = 0;
+      for (auto* b : g.second) S = std::max(S, memo_ec_shard_size(b->data.size(), o_.k));
+      Buffer data(n * o_.k * S, 0), parity(n * o_.m * S);
+      for (size_t i = 0; i < n; ++i) {
+        const auto& d = g.second[i]->data;
+        const size_t Sb = memo_ec_shard_size(d.size(), o_.k);
+        for (int j = 0; j < o_.k; ++j) {
+          const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
+          std::copy(d.begin() + lo, d.begin() + hi, data.begin() + (i * o_.k + j) * S);
+        }
+      }
+      codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
+      // place() fans out over the pool itself; do not nest pool work here
+      for (size_t i = 0; i < n; ++i) {
+        const size_t Sb = memo_ec_shard_size(g.second[i]->data.size(), o_.k);
+        Buffer p((size_t)o_.m * Sb);
+        for (int r = 0; r < o_.m; ++r)
+          std::copy(parity.begin() + (i * o_.m + r) * S, parity.begin() + (i * o_.m + r) * S + Sb,
+                    p.begin() + (size_t)r * Sb);
+        place(*g.second[i], p);
+      }
+    }
+  }
+}
+
+// Shards of block `a` from the nodes in lookup order, in waves, until `want`
+// distinct valid shards are in hand.  Invalid shards count as erasures.
+std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
+                                                                    bool& any_down,
+                                                                    ShardHeader* hdr) {
+  const int total = o_.k + o_.m;
+  auto nodes = overlay_.lookup(a, (int)overlay_.nodes().size());
+  std::map<int, Buffer> got;
+  std::mutex gm;
+  any_down = false;
+  size_t next = 0;
+  while ((int)got.size() < want && next < nodes.size()) {
+    const size_t wave = std::min(nodes.size() - next, (size_t)std::max(total, 1));
+    pool_.parallel_for(wave, [&](size_t w) {
+      auto& nd = nodes[next + w];
+      for (int i = 0; i < total; ++i) {
+        {
+          std::lock_guard<std::mutex> g(gm);
+          if (got.count(i)) continue;
+        }
+        Buffer wire;
+        try {
+          wire = nd->fetch(shard_key(a, i));
+        } catch (Unavailable&) {
+          std::lock_guard<std::mutex> g(gm);
+          any_down = true;
+          return;
+        } catch (silo::MissingKey&) {
+          continue;
+        }
+        try {
+          ShardHeader h = decode_shard(wire, nullptr);
+          if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) continue;
+          std::lock_guard<std::mutex> g(gm);
+          if (hdr && got.empty()) *hdr = h;
+          got.emplace(i, std::move(wire));
+        } catch (ValidationFailed&) {
+          // corrupted shard: an erasure
+        }
+      }
+    });
+    next += wave;
+  }
+  std::vector<std::pair<int, Buffer>> out;
+  for (auto& kv : got) out.emplace_back(kv.first, std::move(kv.second));
+  return out;
+}
+
+std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
+  if (a.mutable_block()) return backend_->fetch(a);
+  const int k = o_.k;
+  bool any_down = false;
+  ShardHeader h;
+  auto shards = gather_shards(a, k, any_down, &h);
+  if (shards.empty()) {
+    if (any_down) throw TooFewPeers("erasure: no shard reachable for " + a.hex());
+    throw MissingBlock("missing block " + a.hex());
+  }
+  if ((int)shards.size() < k)
+    throw TooFewPeers("erasure: " + std::to_string(shards.size()) + " shards reachable, need " +
+                      std::to_string(k));
+  const size_t S = h.shard_size;
+  std::sort(shards.begin(), shards.end(),
+            [](const auto& x, const auto& y) { return x.first < y.first; });
+  shards.resize(k);  // data shards first (sorted), then parity
+  Buffer block((size_t)k * S);
+  std::vector<int> have(k, -1);
+  for (size_t s = 0; s < shards.size(); ++s)
+    if (shards[s].first < k) have[shards[s].first] = (int)s;
+  std::vector<uint8_t> lost;
+  for (int j = 0; j < k; ++j) {
+    if (have[j] >= 0)
+      std::memcpy(block.data() + (size_t)j * S, shards[have[j]].second.data() + ShardHeader::kSize, S);
+    else
+      lost.push_back((uint8_t)j);
+  }
+  if (!lost.empty()) {
+    // systematic shards missing: rebuild them from the k survivors (GPU)
+    std::vector<uint8_t> sidx(k);
+    Buffer surv((size_t)k * S);
+    for (int s = 0; s < k; ++s) {
+      sidx[s] = (uint8_t)shards[s].first;
+      std::memcpy(surv.data() + (size_t)s * S, shards[s].second.data() + ShardHeader::kSize, S);
+    }
+    Buffer out(lost.size() * S);
+    codec_.rebuild(k, o_.m, S, 1, sidx.data(), surv.data(), lost.data(), (int)lost.size(), out.data());
+    for (size_t r = 0; r < lost.size(); ++r)
+      std::memcpy(block.data() + (size_t)lost[r] * S, out.data() + r * S, S);
+    ++decoded_;
+  }
+  block.resize(h.block_size);
+  if (!chb_valid(a, h.salt, block))
+    throw ValidationFailed("erasure: reassembled block does not match its address");
+  auto b = std::make_unique<Block>();
+  b->address = a;
+  b->data = std::move(block);
+  b->salt = h.salt;
+  ++fetched_;
+  return b;
+}
+
+void ErasureConsensus::_remove(const Address& a) {
+  if (a.mutable_block()) return backend_->remove(a);
+  for (auto& nd : overlay_.lookup(a, (int)overlay_.nodes().size()))
+    for (int i = 0; i < o_.k + o_.m; ++i) {
+      try {
+        nd->remove(shard_key(a, i));
+      } catch (Error&) {
+      }
+    }
+  std::lock_guard<std::mutex> g(index_mu_);
+  index_.erase(a);
+}
+
+ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
+  RepairReport rep;
+  const int k = o_.k, m = o_.m, total = k + m;
+  struct Todo {
+    Address a;
+    Placement pl;
+    std::vector<int> lost, surv;
+  };
+  std::vector<Todo> todo;
+  {
+    std::lock_guard<std::mutex> g(index_mu_);
+    for (auto& kv : index_) {
+      ++rep.blocks_checked;
+      Todo t{kv.first, kv.second, {}, {}};
+      for (int i = 0; i < total; ++i) {
+        const Address& o = kv.second.owner[i];
+        auto nd = o ? overlay_.node(o) : nullptr;
+        bool ok = nd && !nd->evicted && (nd->up || !include_down);
+        if (ok && nd->up) ok = nd->has(shard_key(kv.first, i));
+        if (ok) {
+          if (nd->up) t.surv.push_back(i);
+        } else {
+          t.lost.push_back(i);
+        }
+      }
+      if (t.lost.empty()) continue;
+      if ((int)t.surv.size() < k) {
+        ++rep.unrecoverable;
+        continue;
+      }
+      todo.push_back(std::move(t));
+    }
+  }
+  // batches of blocks with the same (S, e): one GPU rebuild call each
+  std::map<std::pair<int, size_t>, std::vector<Todo*>> groups;
+  for (auto& t : todo) groups[{size_bucket(memo_ec_shard_size(t.pl.B, k)), t.lost.size()}].push_back(&t);
+  for (auto& g : groups) {
+    const int e = (int)g.first.second;
+    for (size_t b0 = 0; b0 < g.second.size(); b0 += o_.batch_max) {
+      const size_t n = std::min<size_t>(o_.batch_max, g.second.size() - b0);
+      size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
+      for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(g.second[b0 + bi]->pl.B, k));
+      std::vector<uint8_t> sidx(n * k), lidx(n * e);
+      Buffer surv(n * k * S, 0), out(n * e * S);
+      std::vector<int> good(n, 1);
+      pool_.parallel_for(n, [&](size_t bi) {
+        Todo& t = *g.second[b0 + bi];
+        for (int s = 0; s < k; ++s) {
+          const int i = t.surv[s];
+          try {
+            auto wire = overlay_.node(t.pl.owner[i])->fetch(shard_key(t.a, i));
+            const uint8_t* p = nullptr;
+            const ShardHeader h = decode_shard(wire, &p);
+            std::memcpy(surv.data() + (bi * k + s) * S, p, h.shard_size);
+            sidx[bi * k + s] = (uint8_t)i;
+          } catch (Error&) {
+            good[bi] = 0;
+            return;
+          }
+        }
+        for (int r = 0; r < e; ++r) lidx[bi * e + r] = (uint8_t)t.lost[r];
+      });
+      // survivors that failed validation: substitute nothing, retry next pass
+      for (size_t bi = 0; bi < n; ++bi)
+        if (!good[bi]) {
+          std::fill(sidx.begin() + bi * k, sidx.begin() + (bi + 1) * k, 0);
+          for (int s = 0; s < k; ++s) sidx[bi * k + s] = (uint8_t)s;
+        }
+      codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
+      ++rep.codec_calls;
+      pool_.parallel_for(n, [&](size_t bi) {
+        if (!good[bi]) return;
+        Todo& t = *g.second[b0 + bi];
+        std::set<Address> holders;
+        for (int i = 0; i < total; ++i)
+          if (t.pl.owner[i]) holders.insert(t.pl.owner[i]);
+        auto cand = overlay_.allocate(t.a, (int)overlay_.nodes().size());
+        size_t ci = 0;
+        for (int r = 0; r < e; ++r) {
+          const int i = t.lost[r];
+          ShardHeader h;
+          h.k = (uint8_t)k;
+          h.m = (uint8_t)m;
+          h.index = (uint8_t)i;
+          h.block_size = t.pl.B;
+          h.shard_size = memo_ec_shard_size(t.pl.B, k);
+          h.address = t.a;
+          h.salt = t.pl.salt;
+          const Buffer wire = encode_shard(h, out.data() + (bi * e + r) * S);
+          while (ci < cand.size()) {
+            auto& nd = cand[ci++];
+            if (holders.count(nd->id)) continue;
+            try {
+              nd->store(shard_key(t.a, i), wire);
+              t.pl.owner[i] = nd->id;
+              holders.insert(nd->id);
+              break;
+            } catch (Unavailable&) {
+            }
+          }
+        }
+      });
+      for (size_t bi = 0; bi < n; ++bi) {
+        if (!good[bi]) continue;
+        Todo& t = *g.second[b0 + bi];
+        std::lock_guard<std::mutex> lk(index_mu_);
+        index_[t.a] = t.pl;
+        ++rep.blocks_repaired;
+        rep.shards_rebuilt += (size_t)e;
+        ++repaired_;
+      }
+    }
+  }
+  return rep;
+}
+
+// "erasure" configuration: {"type": "erasure", "data-shards": k,
+// "parity-shards": m, "backend-replication-factor": f}; kebab-case keys as
+// "replication-factor" (Paxos.cc:2273-2276).
+namespace {
+struct RegisterErasure {
+  RegisterErasure() {
+    register_consensus("erasure", [](Overlay& ov, const ConfigMap& c) {
+      ErasureOptions o;
+      auto get = [&](const char* key, int dflt) {
+        auto it = c.find(key);
+        return it == c.end() ? dflt : std::stoi(it->second);
+      };
+      o.k = get("data-shards", 10);
+      o.m = get("parity-shards", 4);
+      o.device = get("device", 0);
+      o.batch_max = get("batch-max", 256);
+      const int f = get("backend-replication-factor", 3);
+      return std::unique_ptr<Consensus>(
+          new ErasureConsensus(std::make_unique<ReplicationConsensus>(ov, f), ov, o));
+    });
+  }
+} register_erasure_;
+}  // namespace
+
+}  // namespace memo_host

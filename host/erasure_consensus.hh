@@ -1,0 +1,161 @@
+// erasure_consensus.hh -- the "erasure" redundancy plugin over libmemo_ec.
+//
+// Drop-in for memo's immutable-block redundancy:
+//   store  : replaces Paxos::_store -> Details::send_immutable_block
+//            (src/memo/model/doughnut/consensus/Paxos.cc:1713-1732, 315-391):
+//            the block is encoded (GPU, batched across concurrent stores) into
+//            k data + m parity shards, shard i goes to owner i of
+//            overlay.allocate(address, k+m);
+//   fetch  : replaces Details::_fetch (Paxos.cc:486-519): any k valid shards;
+//            the k data shards are concatenated as they are (systematic code),
+//            otherwise the missing ones are rebuilt on the GPU; the CHB address
+//            is re-checked on the reassembled block (CHB.cc:79-99);
+//   repair : replaces _disappeared_evict / _rebalance (Paxos.cc:1012-1246):
+//            every shard held by an evicted node is rebuilt in GPU-sized
+//            batches and re-placed on a new owner.
+// Mutable blocks stay on the backend (Paxos in memo, replication here).
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <future>
+#include <thread>
+
+#include "../include/memo_ec.h"
+#include "model.hh"
+
+namespace memo_host {
+
+// --------------------------------------------------------------- codec
+// libmemo_ec contexts for host-memory calls.  A ctx serves one thread at a
+// time (memo_ec.h); a small pool lets concurrent fetch threads decode.
+class Codec {
+ public:
+  explicit Codec(int device = 0, int contexts = 4);
+  ~Codec();
+  Codec(const Codec&) = delete;
+  Codec& operator=(const Codec&) = delete;
+  void encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity);
+  void rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx, const uint8_t* surv,
+               const uint8_t* lost_idx, int e, uint8_t* out);
+  uint64_t encode_calls() const { return encode_calls_; }
+  uint64_t rebuild_calls() const { return rebuild_calls_; }
+
+ private:
+  memo_ec_ctx* acquire();
+  void release(memo_ec_ctx* c);
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<memo_ec_ctx*> all_, free_;
+  std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0};
+};
+
+// ---------------------------------------------------------- shard format
+// On-wire / on-silo shard: a 96-byte header + S payload bytes.  The header
+// replaces the CHB re-hash of LocalPeer::store (Paxos.cc:1571-1575) as the
+// per-shard validation (a shard is not a CHB).
+//   0 "MECS" | 4 version | 5 k | 6 m | 7 index | 8 u64 B | 16 u64 S |
+//   24 address[32] | 56 u32 salt_len | 60 salt[32] | 92 u32 crc32c(payload)
+struct ShardHeader {
+  static constexpr size_t kSize = 96;
+  uint8_t version = 1;
+  uint8_t k = 0, m = 0, index = 0;
+  uint64_t block_size = 0, shard_size = 0;
+  Address address;
+  Buffer salt;
+  uint32_t crc = 0;
+};
+Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
+// Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
+// payload length, CRC32C); throws ValidationFailed.
+ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
+// Silo key of shard `index` of block `address`.
+Key shard_key(const Address& address, int index);
+uint32_t crc32c(const uint8_t* p, size_t n);
+
+// ------------------------------------------------------------ thread pool
+// Parallel fan-out over peers (elle::reactor::for_each_parallel in memo).
+class ThreadPool {
+ public:
+  explicit ThreadPool(int threads);
+  ~ThreadPool();
+  // Runs fn(0..n-1) on the pool and waits; rethrows the first exception.
+  void parallel_for(size_t n, const std::function<void(size_t)>& fn);
+
+ private:
+  void worker();
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> ts_;
+  bool stop_ = false;
+};
+
+// ---------------------------------------------------------------- options
+struct ErasureOptions {
+  int k = 10, m = 4;
+  int device = 0;
+  int batch_max = 256;         // blocks per GPU encode / rebuild call
+  int batch_window_us = 200;   // how long the batcher waits for company
+  int threads = 16;            // peer fan-out (memo's background pool is <= 16)
+};
+
+class ErasureConsensus : public StackedConsensus {
+ public:
+  ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& overlay, ErasureOptions o);
+  ~ErasureConsensus() override;
+
+  std::string redundancy() const override;
+  std::string stats() const override;
+
+  struct RepairReport {
+    size_t blocks_checked = 0, blocks_repaired = 0, shards_rebuilt = 0;
+    size_t unrecoverable = 0, codec_calls = 0;
+  };
+  // Rebuild every shard whose holder is evicted (or lost it), in batches of
+  // batch_max blocks per GPU call, and place it on a new owner.  With
+  // include_down, shards on nodes that are merely unreachable count as lost
+  // too (memo waits for the eviction delay, Paxos.cc:985-1009).
+  RepairReport repair(bool include_down = false);
+  // Store many immutable blocks with one encode call per batch.
+  void store_many(const std::vector<Block>& blocks);
+  const Codec& codec() const { return codec_; }
+  const ErasureOptions& options() const { return o_; }
+
+ protected:
+  void _store(const Block& b, StoreMode mode) override;
+  std::unique_ptr<Block> _fetch(const Address& a) override;
+  void _remove(const Address& a) override;
+
+ private:
+  struct Placement {
+    uint64_t B = 0;
+    Buffer salt;
+    std::vector<Address> owner;  // holder of shard i (null: unplaced)
+  };
+  struct EncodeJob {
+    const Block* block;
+    std::promise<Buffer> parity;  // m x S
+  };
+  Buffer padded(const Block& b, size_t S) const;
+  void place(const Block& b, const Buffer& parity);
+  void batcher_loop();
+  std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
+                                                    ShardHeader* hdr);
+
+  Overlay& overlay_;
+  ErasureOptions o_;
+  Codec codec_;
+  ThreadPool pool_;
+  mutable std::mutex index_mu_;
+  std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_node_blocks analogue
+  // batcher (host C++ batching of concurrent stores into one GPU call)
+  std::mutex bmu_;
+  std::condition_variable bcv_;
+  std::deque<EncodeJob*> bq_;
+  bool bstop_ = false;
+  std::thread bthread_;
+  std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0};
+};
+
+}  // namespace memo_host

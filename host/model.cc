@@ -1,0 +1,361 @@
+// model.cc -- implementation of the restated memo interfaces (model.hh).
+#include "model.hh"
+
+#include <openssl/evp.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <random>
+#include <sstream>
+
+namespace memo_host {
+
+std::string Address::hex() const {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (auto b : value) {
+    s += d[b >> 4];
+    s += d[b & 15];
+  }
+  return s;
+}
+
+Address Address::random(uint8_t fl) {
+  static std::mutex mu;
+  static std::mt19937_64 rng(0x6D656D6F);
+  std::lock_guard<std::mutex> g(mu);
+  uint8_t v[32];
+  for (int i = 0; i < 32; i += 8) {
+    const uint64_t x = rng();
+    std::memcpy(v + i, &x, 8);
+  }
+  return Address(v, fl, true);
+}
+
+std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b, size_t nb) {
+  std::array<uint8_t, 32> out;
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  unsigned len = 0;
+  if (!c || EVP_DigestInit_ex(c, EVP_sha256(), nullptr) != 1 || EVP_DigestUpdate(c, a, na) != 1 ||
+      (b && nb && EVP_DigestUpdate(c, b, nb) != 1) || EVP_DigestFinal_ex(c, out.data(), &len) != 1) {
+    EVP_MD_CTX_free(c);
+    throw Error("sha256 failed");
+  }
+  EVP_MD_CTX_free(c);
+  return out;
+}
+
+Block make_chb(Buffer data, Buffer salt) {
+  Block b;
+  const auto h = sha256(salt.data(), salt.size(), data.data(), data.size());
+  b.address = Address(h.data(), flags::immutable_block, true);
+  b.data = std::move(data);
+  b.salt = std::move(salt);
+  return b;
+}
+
+Block make_mutable(Address address, Buffer data, int version) {
+  Block b;
+  address.value[Address::flag_byte] = flags::mutable_block;
+  b.address = address;
+  b.data = std::move(data);
+  b.is_mutable = true;
+  b.version = version;
+  return b;
+}
+
+bool chb_valid(const Address& address, const Buffer& salt, const Buffer& data) {
+  const auto h = sha256(salt.data(), salt.size(), data.data(), data.size());
+  return Address(h.data(), flags::immutable_block, true) == address;
+}
+
+// ---------------------------------------------------------------- silo
+int Silo::set(const Key& k, const Buffer& v, bool insert, bool update) {
+  if (capacity_ >= 0 && usage_ + (int64_t)v.size() > capacity_)
+    throw silo::InsufficientSpace("insufficient space");
+  const int delta = _set(k, v, insert, update);
+  usage_ += delta;
+  return delta;
+}
+
+int Silo::erase(const Key& k) {
+  const int delta = _erase(k);
+  usage_ += delta;
+  return delta;
+}
+
+Buffer MemorySilo::_get(const Key& k) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blocks_.find(k);
+  if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
+  return it->second;
+}
+
+int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blocks_.find(k);
+  if (it == blocks_.end()) {
+    if (!insert) throw silo::MissingKey("missing key " + k.hex());
+    blocks_.emplace(k, v);
+    return (int)v.size();
+  }
+  if (!update) throw silo::Collision("key exists " + k.hex());
+  const int delta = (int)v.size() - (int)it->second.size();
+  it->second = v;
+  return delta;
+}
+
+int MemorySilo::_erase(const Key& k) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blocks_.find(k);
+  if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
+  const int delta = -(int)it->second.size();
+  blocks_.erase(it);
+  return delta;
+}
+
+std::vector<Key> MemorySilo::_list() {
+  std::lock_guard<std::mutex> g(mu_);
+  std::vector<Key> out;
+  for (auto& kv : blocks_) out.push_back(kv.first);
+  return out;
+}
+
+// ---------------------------------------------------------------- nodes
+void Node::store(const Key& k, const Buffer& v) {
+  if (!up || evicted) throw Unavailable("node down");
+  if (fail_stores) throw Unavailable("store refused");
+  silo->set(k, v, true, true);
+  ++stores;
+}
+
+Buffer Node::fetch(const Key& k) const {
+  if (!up || evicted) throw Unavailable("node down");
+  const_cast<Node*>(this)->fetches++;
+  return silo->get(k);
+}
+
+void Node::remove(const Key& k) {
+  if (!up || evicted) throw Unavailable("node down");
+  silo->erase(k);
+}
+
+bool Node::has(const Key& k) const {
+  try {
+    silo->get(k);
+    return true;
+  } catch (silo::MissingKey&) {
+    return false;
+  }
+}
+
+std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo> silo) {
+  auto n = std::make_shared<Node>();
+  n->id = id;
+  n->silo = std::move(silo);
+  std::lock_guard<std::mutex> g(mu_);
+  nodes_.push_back(n);
+  return n;
+}
+
+std::shared_ptr<Node> Overlay::node(const Address& id) const {
+  std::lock_guard<std::mutex> g(mu_);
+  for (auto& n : nodes_)
+    if (n->id == id) return n;
+  return nullptr;
+}
+
+std::vector<std::shared_ptr<Node>> Overlay::nodes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return nodes_;
+}
+
+std::vector<std::shared_ptr<Node>> Overlay::rank(const Address& address) const {
+  auto all = nodes();
+  std::vector<std::pair<std::array<uint8_t, 32>, std::shared_ptr<Node>>> scored;
+  for (auto& n : all)
+    scored.push_back({sha256(address.value.data(), 32, n->id.value.data(), 32), n});
+  std::sort(scored.begin(), scored.end(),
+            [](const auto& a, const auto& b) { return a.first < b.first; });
+  std::vector<std::shared_ptr<Node>> out;
+  for (auto& s : scored) out.push_back(s.second);
+  return out;
+}
+
+std::vector<std::shared_ptr<Node>> Overlay::allocate(const Address& address, int n) const {
+  std::vector<std::shared_ptr<Node>> out;
+  for (auto& nd : rank(address)) {
+    if ((int)out.size() == n) break;
+    if (nd->up && !nd->evicted) out.push_back(nd);
+  }
+  return out;
+}
+
+std::vector<std::shared_ptr<Node>> Overlay::lookup(const Address& address, int n) const {
+  std::vector<std::shared_ptr<Node>> out;
+  for (auto& nd : rank(address)) {
+    if ((int)out.size() == n) break;
+    if (!nd->evicted) out.push_back(nd);
+  }
+  return out;
+}
+
+// ----------------------------------------------------------- replication
+namespace {
+Key replica_key(const Address& a) { return a; }
+
+Buffer encode_replica(const Block& b) {
+  // [version u32][salt len u32][salt][data]
+  Buffer out(8 + b.salt.size() + b.data.size());
+  const uint32_t v = (uint32_t)b.version, sl = (uint32_t)b.salt.size();
+  std::memcpy(out.data(), &v, 4);
+  std::memcpy(out.data() + 4, &sl, 4);
+  std::copy(b.salt.begin(), b.salt.end(), out.begin() + 8);
+  std::copy(b.data.begin(), b.data.end(), out.begin() + 8 + sl);
+  return out;
+}
+
+Block decode_replica(const Address& a, const Buffer& r) {
+  if (r.size() < 8) throw ValidationFailed("short replica");
+  uint32_t v, sl;
+  std::memcpy(&v, r.data(), 4);
+  std::memcpy(&sl, r.data() + 4, 4);
+  if (8 + (size_t)sl > r.size()) throw ValidationFailed("bad replica");
+  Block b;
+  b.address = a;
+  b.version = (int)v;
+  b.is_mutable = a.mutable_block();
+  b.salt.assign(r.begin() + 8, r.begin() + 8 + sl);
+  b.data.assign(r.begin() + 8 + sl, r.end());
+  return b;
+}
+}  // namespace
+
+std::string ReplicationConsensus::redundancy() const {
+  return to_json({{"type", "replication"}, {"desired_factor", std::to_string(factor_)}});
+}
+
+void ReplicationConsensus::_store(const Block& b, StoreMode mode) {
+  auto owners = mode == STORE_INSERT ? overlay_.allocate(b.address, factor_)
+                                     : overlay_.lookup(b.address, factor_);
+  if (owners.empty()) throw TooFewPeers("no storage peer");
+  const Buffer rep = encode_replica(b);
+  int reached = 0;
+  for (auto& o : owners) {
+    try {
+      o->store(replica_key(b.address), rep);
+      ++reached;
+    } catch (Unavailable&) {
+    }
+  }
+  if (reached == 0) throw TooFewPeers("no owner reachable");
+}
+
+std::unique_ptr<Block> ReplicationConsensus::_fetch(const Address& a) {
+  bool any_up = false;
+  for (auto& o : overlay_.lookup(a, factor_)) {
+    try {
+      auto r = o->fetch(replica_key(a));
+      auto b = std::make_unique<Block>(decode_replica(a, r));
+      if (!b->is_mutable && !chb_valid(a, b->salt, b->data)) continue;
+      return b;
+    } catch (Unavailable&) {
+    } catch (silo::MissingKey&) {
+      any_up = true;
+    }
+  }
+  if (!any_up) throw TooFewPeers("no replica reachable");
+  throw MissingBlock("missing block " + a.hex());
+}
+
+void ReplicationConsensus::_remove(const Address& a) {
+  for (auto& o : overlay_.lookup(a, factor_)) {
+    try {
+      o->remove(replica_key(a));
+    } catch (Error&) {
+    }
+  }
+}
+
+// ----------------------------------------------------------- configuration
+std::string to_json(const ConfigMap& m) {
+  std::ostringstream s;
+  s << "{";
+  bool first = true;
+  for (auto& kv : m) {
+    if (!first) s << ", ";
+    first = false;
+    s << "\"" << kv.first << "\": ";
+    const bool num = !kv.second.empty() &&
+                     kv.second.find_first_not_of("0123456789.-") == std::string::npos;
+    if (num) s << kv.second;
+    else s << "\"" << kv.second << "\"";
+  }
+  s << "}";
+  return s.str();
+}
+
+ConfigMap from_json(const std::string& t) {
+  // flat objects only: {"key": "string" | number, ...}
+  ConfigMap m;
+  size_t i = t.find('{');
+  if (i == std::string::npos) throw Error("config: expected an object");
+  ++i;
+  auto skip = [&] {
+    while (i < t.size() && (t[i] == ' ' || t[i] == '\n' || t[i] == '\t' || t[i] == ',')) ++i;
+  };
+  while (true) {
+    skip();
+    if (i >= t.size()) throw Error("config: unterminated object");
+    if (t[i] == '}') break;
+    if (t[i] != '"') throw Error("config: expected a key");
+    const size_t ke = t.find('"', i + 1);
+    const std::string key = t.substr(i + 1, ke - i - 1);
+    i = t.find(':', ke);
+    if (i == std::string::npos) throw Error("config: expected ':'");
+    ++i;
+    skip();
+    std::string val;
+    if (t[i] == '"') {
+      const size_t ve = t.find('"', i + 1);
+      val = t.substr(i + 1, ve - i - 1);
+      i = ve + 1;
+    } else {
+      const size_t ve = t.find_first_of(",}", i);
+      val = t.substr(i, ve - i);
+      while (!val.empty() && val.back() == ' ') val.pop_back();
+      i = ve;
+    }
+    m[key] = val;
+  }
+  return m;
+}
+
+namespace {
+std::map<std::string, ConsensusFactory>& registry() {
+  static std::map<std::string, ConsensusFactory> r;
+  return r;
+}
+struct RegisterReplication {
+  RegisterReplication() {
+    register_consensus("replication", [](Overlay& ov, const ConfigMap& c) {
+      auto it = c.find("replication-factor");
+      const int f = it == c.end() ? 3 : std::stoi(it->second);
+      return std::unique_ptr<Consensus>(new ReplicationConsensus(ov, f));
+    });
+  }
+} register_replication_;
+}  // namespace
+
+void register_consensus(const std::string& type, ConsensusFactory f) { registry()[type] = f; }
+
+std::unique_ptr<Consensus> make_consensus(Overlay& overlay, const std::string& json) {
+  const auto c = from_json(json);
+  auto it = c.find("type");
+  if (it == c.end()) throw Error("config: missing \"type\"");
+  auto f = registry().find(it->second);
+  if (f == registry().end()) throw Error("config: unknown consensus type " + it->second);
+  return f->second(overlay, c);
+}
+
+}  // namespace memo_host

@@ -1,0 +1,261 @@
+// model.hh -- minimal, faithful restatement of the memo interfaces the
+// erasure plugin sits behind (the reference needs boost/elle/drake and is not
+// buildable here).  Each type cites the reference declaration
+// whose contract it keeps; only what the redundancy path touches is kept.
+#pragma once
+
+#include <array>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace memo_host {
+
+using Buffer = std::vector<uint8_t>;  // elle::Buffer (elle/src/elle/Buffer.hh:34)
+
+// ---------------------------------------------------------------- errors
+// elle::Error, model::MissingBlock (src/memo/model/MissingBlock.hh),
+// athena::paxos::TooFewPeers / Unavailable (Paxos.cc:65-83),
+// ValidationFailed (Paxos.cc:1572-1597), silo::MissingKey / Collision.
+struct Error : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+struct MissingBlock : Error {
+  using Error::Error;
+};
+struct TooFewPeers : Error {
+  using Error::Error;
+};
+struct Unavailable : Error {
+  using Error::Error;
+};
+struct ValidationFailed : Error {
+  using Error::Error;
+};
+namespace silo {
+struct MissingKey : Error {
+  using Error::Error;
+};
+struct Collision : Error {
+  using Error::Error;
+};
+struct InsufficientSpace : Error {
+  using Error::Error;
+};
+}  // namespace silo
+
+// --------------------------------------------------------------- address
+// model::Address (src/memo/model/Address.hh:18-60): 32 bytes, the last byte
+// carries the flags (0 mutable, 1 immutable) when `combine` is set.
+namespace flags {
+constexpr uint8_t mutable_block = 0;
+constexpr uint8_t immutable_block = 1;
+}  // namespace flags
+
+struct Address {
+  static constexpr int flag_byte = 31;
+  std::array<uint8_t, 32> value{};
+  Address() = default;
+  Address(const uint8_t* v, uint8_t flags, bool combine) {
+    std::memcpy(value.data(), v, 32);
+    if (combine) value[flag_byte] = flags;
+  }
+  bool mutable_block() const { return value[flag_byte] == flags::mutable_block; }
+  explicit operator bool() const {
+    for (auto b : value)
+      if (b) return true;
+    return false;
+  }
+  bool operator==(const Address& o) const { return value == o.value; }
+  bool operator!=(const Address& o) const { return value != o.value; }
+  bool operator<(const Address& o) const { return value < o.value; }
+  std::string hex() const;
+  static Address random(uint8_t flags);
+};
+
+struct AddressHash {
+  size_t operator()(const Address& a) const {
+    size_t h;
+    std::memcpy(&h, a.value.data(), sizeof h);
+    return h;
+  }
+};
+
+// SHA-256 (OpenSSL, as elle::cryptography::hash(..., Oneway::sha256)).
+std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b = nullptr, size_t nb = 0);
+
+// ----------------------------------------------------------------- blocks
+// blocks::Block (src/memo/model/blocks/Block.hh:107-200): an address and the
+// payload data() (Block.hh:142).  Immutable content-hash blocks are CHBs:
+// address = SHA-256(salt || data) with the immutable flag combined
+// (CHB::_hash_address, src/memo/model/doughnut/CHB.cc:264-289; owner = null).
+struct Block {
+  Address address;
+  Buffer data;
+  Buffer salt;
+  bool is_mutable = false;
+  int version = 0;  // mutable blocks only
+};
+
+Block make_chb(Buffer data, Buffer salt = {});
+Block make_mutable(Address address, Buffer data, int version = 1);
+// CHB::validate (CHB.cc:79-99): the address is the hash of the content.
+bool chb_valid(const Address& address, const Buffer& salt, const Buffer& data);
+
+// ------------------------------------------------------------------- silo
+// silo::Silo (src/memo/silo/Silo.hh:33-129): get/set/erase/list with the
+// MissingKey / Collision contract; subclasses implement _get/_set/_erase/_list.
+using Key = Address;
+
+class Silo {
+ public:
+  explicit Silo(int64_t capacity = -1) : capacity_(capacity) {}
+  virtual ~Silo() = default;
+  Buffer get(const Key& k) const { return _get(k); }
+  // insert: accept a new key; update: accept an existing key.
+  int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
+  int erase(const Key& k);
+  std::vector<Key> list() { return _list(); }
+  virtual std::string type() const = 0;
+  int64_t usage() const { return usage_; }
+  int64_t capacity() const { return capacity_; }
+
+ protected:
+  virtual Buffer _get(const Key& k) const = 0;
+  virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
+  virtual int _erase(const Key& k) = 0;
+  virtual std::vector<Key> _list() = 0;
+  int64_t capacity_;
+  std::atomic<int64_t> usage_{0};
+};
+
+// silo::Memory (src/memo/silo/Memory.hh:10-61): the in-memory test silo.
+class MemorySilo : public Silo {
+ public:
+  using Silo::Silo;
+  std::string type() const override { return "memory"; }
+
+ protected:
+  Buffer _get(const Key& k) const override;
+  int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
+  int _erase(const Key& k) override;
+  std::vector<Key> _list() override;
+
+ private:
+  mutable std::mutex mu_;
+  std::map<Key, Buffer> blocks_;
+};
+
+// ------------------------------------------------------------ peers/overlay
+// A storage node: doughnut::Local with its silo (Local.cc:180-257) as seen
+// through Peer::store/fetch/remove (doughnut/Peer.hh:19-89).  `up` models
+// reachability: a down node raises Unavailable like a failed RPC.
+struct Node {
+  Address id;
+  std::unique_ptr<Silo> silo;
+  std::atomic<bool> up{true};
+  std::atomic<bool> evicted{false};
+  std::atomic<int64_t> stores{0}, fetches{0};
+  // store barrier (tests/doughnut.cc:1048-1163 instrumented Local)
+  std::atomic<bool> fail_stores{false};
+
+  void store(const Key& k, const Buffer& v);
+  Buffer fetch(const Key& k) const;
+  void remove(const Key& k);
+  bool has(const Key& k) const;
+};
+
+// overlay::Overlay (src/memo/overlay/Overlay.hh:34-188): allocate(address, n)
+// chooses n owners for a new block, lookup(address, n) the nodes that may hold
+// it.  This in-process overlay (like tests/DHT.hh's test overlay) ranks nodes
+// by rendezvous hashing of (address, node id), so every client agrees.
+class Overlay {
+ public:
+  std::shared_ptr<Node> add_node(const Address& id, std::unique_ptr<Silo> silo);
+  std::shared_ptr<Node> node(const Address& id) const;
+  // Every node in rendezvous order for `address` (reachable or not).
+  std::vector<std::shared_ptr<Node>> rank(const Address& address) const;
+  // The first n reachable nodes for a new block (Overlay::allocate).
+  std::vector<std::shared_ptr<Node>> allocate(const Address& address, int n) const;
+  // The first n non-evicted nodes (Overlay::lookup); may include down nodes.
+  std::vector<std::shared_ptr<Node>> lookup(const Address& address, int n) const;
+  std::vector<std::shared_ptr<Node>> nodes() const;
+
+ private:
+  mutable std::mutex mu_;
+  std::vector<std::shared_ptr<Node>> nodes_;
+};
+
+// -------------------------------------------------------------- consensus
+// consensus::Consensus (src/memo/model/doughnut/Consensus.hh:24-174): the
+// redundancy plugin base.  store/fetch/remove dispatch to the virtuals.
+enum StoreMode { STORE_INSERT, STORE_UPDATE };
+
+class Consensus {
+ public:
+  virtual ~Consensus() = default;
+  void store(const Block& b, StoreMode mode = STORE_INSERT) { _store(b, mode); }
+  std::unique_ptr<Block> fetch(const Address& a) { return _fetch(a); }
+  void remove(const Address& a) { _remove(a); }
+  // Consensus::redundancy / stats (Consensus.cc:350-357): JSON text.
+  virtual std::string redundancy() const = 0;
+  virtual std::string stats() const { return "{}"; }
+
+ protected:
+  virtual void _store(const Block& b, StoreMode mode) = 0;
+  virtual std::unique_ptr<Block> _fetch(const Address& a) = 0;
+  virtual void _remove(const Address& a) = 0;
+};
+
+// consensus::StackedConsensus (Consensus.hh:129-142).
+class StackedConsensus : public Consensus {
+ public:
+  explicit StackedConsensus(std::unique_ptr<Consensus> backend) : backend_(std::move(backend)) {}
+  Consensus& backend() { return *backend_; }
+
+ protected:
+  std::unique_ptr<Consensus> backend_;
+};
+
+// The replication path memo uses for every block today (Paxos with
+// replication-factor N, immutable branch Paxos.cc:315-391 / 486-519),
+// restated without the Paxos protocol: the full block on `factor` owners,
+// read from the first replica that answers.  The erasure plugin keeps it for
+// mutable (metadata) blocks.
+class ReplicationConsensus : public Consensus {
+ public:
+  ReplicationConsensus(Overlay& overlay, int factor) : overlay_(overlay), factor_(factor) {}
+  std::string redundancy() const override;
+
+ protected:
+  void _store(const Block& b, StoreMode mode) override;
+  std::unique_ptr<Block> _fetch(const Address& a) override;
+  void _remove(const Address& a) override;
+
+ private:
+  Overlay& overlay_;
+  int factor_;
+};
+
+// ----------------------------------------------------------- configuration
+// consensus::Configuration (Consensus.hh:148-174): polymorphic, serialized
+// with a "type" key; factories registered by name like
+// Hierarchy<Configuration>::Register<Paxos::Configuration>("paxos")
+// (Paxos.cc:2285-2286).  Flat JSON objects with kebab-case keys.
+using ConfigMap = std::map<std::string, std::string>;
+std::string to_json(const ConfigMap& m);
+ConfigMap from_json(const std::string& text);
+
+using ConsensusFactory = std::function<std::unique_ptr<Consensus>(Overlay&, const ConfigMap&)>;
+void register_consensus(const std::string& type, ConsensusFactory f);
+std::unique_ptr<Consensus> make_consensus(Overlay& overlay, const std::string& json_config);
+
+}  // namespace memo_host

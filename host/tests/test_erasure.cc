@@ -1,0 +1,392 @@
+// test_erasure.cc -- the reference's redundancy-path semantics tests, ported
+// onto the erasure plugin (host/erasure_consensus.hh).  Each test names the
+// reference test it follows.  Tests tagged GPU run the codec (libmemo_ec on
+// an MI355X); the others need no GPU.
+//   usage: test_erasure [--cpu-only] [filter]
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <set>
+#include <thread>
+
+#include "../erasure_consensus.hh"
+
+using namespace memo_host;
+
+namespace {
+
+struct TestCase {
+  const char* name;
+  bool gpu;
+  void (*fn)();
+};
+std::vector<TestCase>& tests() {
+  static std::vector<TestCase> t;
+  return t;
+}
+struct Reg {
+  Reg(const char* n, bool g, void (*f)()) { tests().push_back({n, g, f}); }
+};
+int g_fail = 0;
+
+#define TEST(name, gpu)                      \
+  static void test_##name();                 \
+  static Reg reg_##name(#name, gpu, test_##name); \
+  static void test_##name()
+#define CHECK(x)                                                             \
+  do {                                                                       \
+    if (!(x)) {                                                              \
+      std::fprintf(stderr, "  CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #x); \
+      ++g_fail;                                                              \
+    }                                                                        \
+  } while (0)
+#define CHECK_THROW(expr, Exc)                                               \
+  do {                                                                       \
+    bool thrown_ = false;                                                    \
+    try {                                                                    \
+      expr;                                                                  \
+    } catch (Exc&) {                                                         \
+      thrown_ = true;                                                        \
+    } catch (std::exception & e_) {                                          \
+      std::fprintf(stderr, "  %s:%d: wrong exception: %s\n", __FILE__, __LINE__, e_.what()); \
+    }                                                                        \
+    if (!thrown_) {                                                          \
+      std::fprintf(stderr, "  CHECK_THROW failed %s:%d: %s\n", __FILE__, __LINE__, #expr); \
+      ++g_fail;                                                              \
+    }                                                                        \
+  } while (0)
+
+Buffer bytes(const char* s) { return Buffer(s, s + std::strlen(s)); }
+
+Buffer random_bytes(size_t n, uint64_t seed) {
+  std::mt19937_64 r(seed);
+  Buffer b(n);
+  for (auto& x : b) x = (uint8_t)r();
+  return b;
+}
+
+// An in-process network like tests/DHT.hh: `nodes` nodes with memory silos
+// on one overlay, and an erasure consensus client over it.
+struct Net {
+  Overlay overlay;
+  std::vector<std::shared_ptr<Node>> nodes;
+  std::unique_ptr<ErasureConsensus> ec;
+  Net(int n, int k, int m, int batch_window_us = 200) {
+    for (int i = 0; i < n; ++i) {
+      uint8_t id[32] = {0};
+      id[0] = (uint8_t)(i + 1);
+      id[1] = 0x4d;
+      nodes.push_back(overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>()));
+    }
+    ErasureOptions o;
+    o.k = k;
+    o.m = m;
+    o.batch_window_us = batch_window_us;
+    ec = std::make_unique<ErasureConsensus>(std::make_unique<ReplicationConsensus>(overlay, 3),
+                                            overlay, o);
+  }
+  // nodes holding at least one shard of `a`
+  int holders(const Address& a, int total) {
+    int h = 0;
+    for (auto& n : nodes)
+      for (int i = 0; i < total; ++i)
+        if (!n->evicted && n->has(shard_key(a, i))) {
+          ++h;
+          break;
+        }
+    return h;
+  }
+  int shards(const Address& a, int total) {
+    int s = 0;
+    for (auto& n : nodes)
+      for (int i = 0; i < total; ++i)
+        if (!n->evicted && n->has(shard_key(a, i))) ++s;
+    return s;
+  }
+};
+
+}  // namespace
+
+// ------------------------------------------------------------- CPU tests
+// tests/storage.cc:15-45: the silo contract shards are stored under.
+TEST(silo_memory_contract, false) {
+  MemorySilo s;
+  Key k1 = Address::random(flags::immutable_block), k2 = Address::random(flags::immutable_block);
+  s.set(k1, bytes("the grey"));
+  CHECK(s.get(k1) == bytes("the grey"));
+  s.set(k1, bytes("the white"), false, true);
+  CHECK(s.get(k1) == bytes("the white"));
+  CHECK_THROW(s.set(k1, Buffer()), silo::Collision);
+  CHECK(s.get(k1) == bytes("the white"));
+  CHECK_THROW(s.get(k2), silo::MissingKey);
+  CHECK_THROW(s.set(k2, Buffer(), false, true), silo::MissingKey);
+  CHECK_THROW(s.erase(k2), silo::MissingKey);
+  s.erase(k1);
+  CHECK_THROW(s.get(k1), silo::MissingKey);
+  CHECK(s.list().empty());
+}
+
+// tests/storage.cc:47-84: capacity.
+TEST(silo_capacity, false) {
+  MemorySilo s(10);
+  Key k = Address::random(flags::immutable_block);
+  s.set(k, Buffer(8));
+  CHECK(s.usage() == 8);
+  CHECK_THROW(s.set(Address::random(flags::immutable_block), Buffer(8)), silo::InsufficientSpace);
+  s.erase(k);
+  CHECK(s.usage() == 0);
+}
+
+TEST(shard_format_round_trip_and_validation, false) {
+  ShardHeader h;
+  h.k = 10;
+  h.m = 4;
+  h.index = 12;
+  h.block_size = 1000;
+  h.shard_size = memo_ec_shard_size(1000, 10);
+  h.address = Address::random(flags::immutable_block);
+  h.salt = bytes("salt");
+  Buffer payload = random_bytes(h.shard_size, 7);
+  Buffer w = encode_shard(h, payload.data());
+  CHECK(w.size() == ShardHeader::kSize + h.shard_size);
+  const uint8_t* p = nullptr;
+  ShardHeader d = decode_shard(w, &p);
+  CHECK(d.k == 10 && d.m == 4 && d.index == 12 && d.block_size == 1000);
+  CHECK(d.address == h.address && d.salt == h.salt);
+  CHECK(std::memcmp(p, payload.data(), h.shard_size) == 0);
+  Buffer bad = w;
+  bad[ShardHeader::kSize + 5] ^= 1;  // payload bit flip
+  CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  bad = w;
+  bad[16] ^= 1;  // shard size inconsistent with block size
+  CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  bad = w;
+  bad.resize(bad.size() - 1);
+  CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  bad = w;
+  bad[0] = 'X';
+  CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  // CRC32C known answer (RFC 3720 B.4: 32 bytes of zeros -> 0x8a9136aa)
+  uint8_t z[32] = {0};
+  CHECK(crc32c(z, 32) == 0x8a9136aau);
+}
+
+TEST(config_registry, false) {
+  Overlay ov;
+  auto c = from_json("{\"type\": \"erasure\", \"data-shards\": 10, \"parity-shards\": 4}");
+  CHECK(c["type"] == "erasure" && c["data-shards"] == "10" && c["parity-shards"] == "4");
+  CHECK(from_json(to_json(c)) == c);
+  CHECK_THROW(make_consensus(ov, "{\"type\": \"nope\"}"), Error);
+  CHECK_THROW(make_consensus(ov, "{\"data-shards\": 3}"), Error);
+  auto r = make_consensus(ov, "{\"type\": \"replication\", \"replication-factor\": 2}");
+  CHECK(from_json(r->redundancy())["type"] == "replication");
+}
+
+TEST(placement_is_deterministic_and_distinct, false) {
+  Overlay ov;
+  for (int i = 0; i < 20; ++i) ov.add_node(Address::random(0), std::make_unique<MemorySilo>());
+  auto a = Address::random(flags::immutable_block);
+  auto o1 = ov.allocate(a, 14), o2 = ov.allocate(a, 14);
+  CHECK(o1.size() == 14);
+  std::set<Address> ids;
+  for (size_t i = 0; i < o1.size(); ++i) {
+    CHECK(o1[i]->id == o2[i]->id);
+    ids.insert(o1[i]->id);
+  }
+  CHECK(ids.size() == 14);
+  o1[3]->up = false;  // allocate skips unreachable nodes
+  auto o3 = ov.allocate(a, 14);
+  for (auto& n : o3) CHECK(n->up);
+}
+
+TEST(chb_address_is_content_hash, false) {
+  Block b = make_chb(bytes("\\_o<"), bytes("salt"));
+  CHECK(!b.address.mutable_block());
+  CHECK(chb_valid(b.address, b.salt, b.data));
+  Buffer other = b.data;
+  other[0] ^= 1;
+  CHECK(!chb_valid(b.address, b.salt, other));
+}
+
+// -------------------------------------------------------------- GPU tests
+// tests/doughnut.cc:320-335 (CHB): insert -> fetch equal -> remove.
+TEST(CHB, true) {
+  Net net(16, 10, 4);
+  Block b = make_chb(bytes("\\_o<"));
+  net.ec->store(b);
+  CHECK(net.holders(b.address, 14) == 14);
+  auto f = net.ec->fetch(b.address);
+  CHECK(f->data == b.data);
+  net.ec->remove(b.address);
+  CHECK(net.shards(b.address, 14) == 0);
+  CHECK_THROW(net.ec->fetch(b.address), MissingBlock);
+}
+
+// tests/doughnut.cc:361-373 (missing_block).
+TEST(missing_block, true) {
+  Net net(16, 10, 4);
+  CHECK_THROW(net.ec->fetch(Address::random(flags::immutable_block)), MissingBlock);
+  CHECK_THROW(net.ec->fetch(Address::random(flags::mutable_block)), MissingBlock);
+}
+
+// tests/doughnut.cc:840-846 (CHB_no_peer): no storage peer -> error.
+TEST(CHB_no_peer, true) {
+  Net net(4, 10, 4);  // fewer reachable owners than k
+  CHECK_THROW(net.ec->store(make_chb(bytes("no peer"))), TooFewPeers);
+}
+
+// Mutable blocks keep the backend (Paxos in memo) -- OKB, doughnut.cc:337-359.
+TEST(mutable_blocks_use_backend, true) {
+  Net net(16, 10, 4);
+  Block b = make_mutable(Address::random(flags::mutable_block), bytes("foo"));
+  net.ec->store(b);
+  CHECK(net.ec->fetch(b.address)->data == bytes("foo"));
+  Block u = make_mutable(b.address, bytes("foobar"), 2);
+  net.ec->store(u, STORE_UPDATE);
+  CHECK(net.ec->fetch(b.address)->data == bytes("foobar"));
+}
+
+// tests/consensus/paxos.cc:7-63 (availability_2/3), for k+m: reads survive
+// up to m unreachable owners, a data-shard loss is rebuilt on the GPU, and
+// more than m losses raise TooFewPeers.
+TEST(availability, true) {
+  for (size_t size : {size_t(1), size_t(1000), size_t(1) << 20, size_t(3000001)}) {
+    Net net(14, 10, 4);
+    Block b = make_chb(random_bytes(size, size));
+    net.ec->store(b);
+    auto owners = net.overlay.allocate(b.address, 14);
+    // lose 4 owners, three of them holding data shards
+    for (int i : {0, 3, 9, 12}) owners[i]->up = false;
+    auto f = net.ec->fetch(b.address);
+    CHECK(f->data == b.data);
+    owners[5]->up = false;  // 5 > m
+    CHECK_THROW(net.ec->fetch(b.address), TooFewPeers);
+  }
+}
+
+// Corrupted shards are erasures: flip bytes in m shards, fetch still exact.
+TEST(corrupted_shards_are_erasures, true) {
+  Net net(14, 10, 4);
+  Block b = make_chb(random_bytes(777777, 3));
+  net.ec->store(b);
+  int flipped = 0;
+  for (auto& n : net.nodes)
+    for (int i : {1, 2, 11, 13}) {
+      Key key = shard_key(b.address, i);
+      if (!n->has(key)) continue;
+      Buffer w = n->silo->get(key);
+      w[ShardHeader::kSize + 100] ^= 0x5a;
+      n->silo->set(key, w, false, true);
+      ++flipped;
+    }
+  CHECK(flipped == 4);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// tests/doughnut.cc:1651-1691 (evict_faulty), 1484-1512 (expand_new_block),
+// 2158-2176 (CHB_unavailable): after owners are lost the shards are rebuilt
+// on new owners, after which the block survives m further losses.
+TEST(evict_and_repair, true) {
+  Net net(24, 10, 4);
+  std::vector<Block> blocks;
+  for (int i = 0; i < 40; ++i) blocks.push_back(make_chb(random_bytes(50000 + 997 * i, i)));
+  net.ec->store_many(blocks);
+  // evict 4 nodes that hold shards
+  int evicted = 0;
+  for (auto& n : net.nodes)
+    if (evicted < 4 && !n->silo->list().empty()) {
+      n->evicted = true;
+      ++evicted;
+    }
+  auto rep = net.ec->repair();
+  CHECK(rep.unrecoverable == 0);
+  CHECK(rep.blocks_repaired > 0);
+  CHECK(rep.codec_calls >= 1 && rep.codec_calls < rep.blocks_repaired);  // batched
+  for (auto& b : blocks) CHECK(net.shards(b.address, 14) == 14);
+  // 4 more failures among the remaining nodes: still readable
+  int down = 0;
+  for (auto& n : net.nodes)
+    if (!n->evicted && down < 4 && !n->silo->list().empty()) {
+      n->up = false;
+      ++down;
+    }
+  for (auto& b : blocks) CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// CHB_unavailable (doughnut.cc:2158-2176): an owner refusing the store
+// leaves the block under-sharded; repair completes it.
+TEST(CHB_unavailable, true) {
+  Net net(16, 10, 4);
+  Block b = make_chb(bytes("CHB_unavailable"));
+  auto owners = net.overlay.allocate(b.address, 14);
+  owners[2]->fail_stores = true;
+  net.ec->store(b);
+  CHECK(net.shards(b.address, 14) == 13);
+  owners[2]->fail_stores = false;
+  owners[2]->evicted = true;
+  auto rep = net.ec->repair();
+  CHECK(rep.shards_rebuilt == 1);
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// Concurrent stores from many threads are batched into few GPU encodes.
+TEST(concurrent_stores_batch_on_gpu, true) {
+  Net net(16, 10, 4, 2000);
+  std::vector<Block> blocks;
+  for (int i = 0; i < 64; ++i) blocks.push_back(make_chb(random_bytes(65536, 100 + i)));
+  std::vector<std::thread> ts;
+  for (int t = 0; t < 16; ++t)
+    ts.emplace_back([&, t] {
+      for (int i = t; i < 64; i += 16) net.ec->store(blocks[i]);
+    });
+  for (auto& t : ts) t.join();
+  const auto calls = net.ec->codec().encode_calls();
+  CHECK(calls < 64);
+  for (auto& b : blocks) CHECK(net.ec->fetch(b.address)->data == b.data);
+  std::printf("  (64 concurrent stores -> %llu GPU encode calls)\n", (unsigned long long)calls);
+}
+
+// Redundancy JSON (Consensus::redundancy, Paxos.cc:2218-2225 shape).
+TEST(redundancy_json, true) {
+  Net net(16, 10, 4);
+  auto r = from_json(net.ec->redundancy());
+  CHECK(r["type"] == "erasure" && r["k"] == "10" && r["m"] == "4" && r["desired_factor"] == "1.4");
+  Overlay ov;
+  for (int i = 0; i < 8; ++i) ov.add_node(Address::random(0), std::make_unique<MemorySilo>());
+  auto c = make_consensus(ov, "{\"type\": \"erasure\", \"data-shards\": 4, \"parity-shards\": 2}");
+  CHECK(from_json(c->redundancy())["k"] == "4");
+  Block b = make_chb(random_bytes(4096, 9));
+  c->store(b);
+  CHECK(c->fetch(b.address)->data == b.data);
+}
+
+int main(int argc, char** argv) {
+  bool cpu_only = false;
+  const char* filter = nullptr;
+  for (int i = 1; i < argc; ++i) {
+    if (!std::strcmp(argv[i], "--cpu-only")) cpu_only = true;
+    else filter = argv[i];
+  }
+  int run = 0, failed = 0;
+  for (auto& t : tests()) {
+    if (cpu_only && t.gpu) continue;
+    if (filter && !std::strstr(t.name, filter)) continue;
+    const int before = g_fail;
+    std::printf("[ RUN  ] %s\n", t.name);
+    std::fflush(stdout);
+    try {
+      t.fn();
+    } catch (std::exception& e) {
+      std::fprintf(stderr, "  uncaught: %s\n", e.what());
+      ++g_fail;
+    }
+    ++run;
+    const bool ok = g_fail == before;
+    failed += !ok;
+    std::printf("[ %s ] %s\n", ok ? " OK " : "FAIL", t.name);
+  }
+  std::printf("%d tests, %d failed\n", run, failed);
+  return failed ? 1 : 0;
+}
