@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sweep", action="store_true", help="also run the C5 mixed sweep")
+    ap.add_argument("--sweep-gib", type=float, default=4.0, help="payload GiB per sweep point")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="every rank on cuda:0 (rehearse N>1 on a 1-GPU box with gloo)")
     return ap.parse_args()
 
 
@@ -77,9 +81,50 @@ def timed_launches(torch, fn, steps, warmup, dist, stream):
 def max_over_ranks(torch, dist, x):
     if dist is None:
         return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sweep(torch, ec, codec, stream, gib, steps):
+    """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
+    ~gib GiB of payload per point, one encode launch per step; then the same
+    12 smaller groups fused into one launch (memo_ec_encode_segments)."""
+    points = []
+    for (k, m) in [(4, 2), (10, 4), (16, 4)]:
+        for B in [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20]:
+            S = ec.shard_size(B, k)
+            n = max(1, int(gib * 2**30) // B)
+            d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+            p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+            codec.fill_blocks(SEED, 0, n, B, k, S, d)
+            _, kms = timed_launches(torch, lambda: codec.encode(k, m, d, p), steps, 2, None, stream)
+            ms = float(np.mean(kms))
+            alg = (k + m) * S * n
+            points.append({"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
+                           "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
+                           "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)})
+            del d, p
+    segs, alg, pay = [], 0, 0
+    for (k, m) in [(4, 2), (10, 4), (16, 4)]:
+        for B in [4 << 10, 64 << 10, 1 << 20, 4 << 20]:
+            S = ec.shard_size(B, k)
+            n = max(1, int(gib * 2**30 / 12) // B)
+            d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+            p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+            codec.fill_blocks(SEED, 0, n, B, k, S, d)
+            segs.append((k, m, S, n, d, p))
+            alg += (k + m) * S * n
+            pay += n * B
+    _, kms = timed_launches(torch, lambda: codec.encode_segments(segs), steps, 2, None, stream)
+    ms = float(np.mean(kms))
+    fused = {"segments": len(segs), "kernel_ms": round(ms, 4),
+             "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
+             "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    return {"workload": "BASELINE.json C5: RS(k,m) encode per (k,m) x block size, ~%.1f GiB "
+                        "payload per point; fused = 12 mixed groups in one launch" % gib,
+            "points": points, "fused": fused}
 
 
 def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
@@ -124,14 +169,20 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if args.same_device:
+        local = 0
     if world > 1:
         import torch.distributed as dist_mod
         torch.cuda.set_device(local)
-        dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist_mod.init_process_group(args.dist_backend)
         dist = dist_mod
     else:
         torch.cuda.set_device(0)
     from memo_amd import ec
+    from memo_amd.partition import weak_range
 
     k, m, B, n, e = args.k, args.m, args.block_bytes, args.blocks, args.erasures
     S = ec.shard_size(B, k)
@@ -145,7 +196,8 @@ def main():
 
     data = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
     par = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
-    codec.fill_blocks(SEED, rank * n, n, B, k, S, data)
+    first_block, _ = weak_range(n, rank)  # rank r owns blocks [r*n, (r+1)*n)
+    codec.fill_blocks(SEED, first_block, n, B, k, S, data)
     torch.cuda.synchronize()
 
     enc = lambda: codec.encode(k, m, data, par)  # noqa: E731
@@ -187,7 +239,7 @@ def main():
             pass
 
     if not args.no_rebuild and e > 0:
-        s_idx, l_idx = ec.erasures(SEED, rank * n, n, k, m, e)
+        s_idx, l_idx = ec.erasures(SEED, first_block, n, k, m, e)
         sd = torch.from_numpy(s_idx).cuda()
         ld = torch.from_numpy(l_idx).cuda()
         surv = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
@@ -237,6 +289,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = par[:4].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, sample)
+
+    if args.sweep and world == 1:
+        del data, par
+        result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4))
 
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -15,6 +15,9 @@
 #ifndef MEMO_EC_MAC_WAVES
 #define MEMO_EC_MAC_WAVES 1
 #endif
+#ifndef MEMO_EC_MAC_XCD
+#define MEMO_EC_MAC_XCD 1
+#endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif

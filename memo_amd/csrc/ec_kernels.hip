@@ -292,7 +292,17 @@ __global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const Ma
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
 
   // Segment of this workgroup (uniform), then its tile.
+#if MEMO_EC_MAC_XCD
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so
+  // give XCD x a contiguous range of tiles (bijective for any grid size):
+  // neighbouring tiles, which share the 128-byte lines at their edges when
+  // S is not a multiple of 128, then meet in the same L2.  Speed only.
+  const uint32_t W = gridDim.x, q = W / 8, rr = W % 8;
+  const uint32_t x = blockIdx.x % 8, i8 = blockIdx.x / 8;
+  const uint32_t wg = x * q + (x < rr ? x : rr) + i8;
+#else
   const uint32_t wg = blockIdx.x;
+#endif
   uint32_t sid = 0;
   for (uint32_t s = 1; s < L.nseg; ++s)
     if (wg >= L.seg[s].wg_begin) sid = s;
