@@ -222,3 +222,77 @@ def test_full_size_c2_c3_round_trip(codec, O):
 def ec_erasures(n, k, m, e):
     from memo_amd import ec
     return ec.erasures(SEED, 0, n, k, m, e)
+
+
+def test_hip_graph_capture_replay(codec, O):
+    """Device-resident encode + rebuild captured into one HIP graph (via
+    torch.cuda.CUDAGraph on ROCm) and replayed on new inputs: launch-bound
+    callers can replay instead of re-launching."""
+    import torch
+    k, m, B, n, e = 10, 4, 200000, 24, 3
+    S = O.shard_size(B, k)
+    d = empty(n, k * S)
+    p = empty(n, m * S)
+    s, l = O.erasures(SEED, 0, n, k, m, e)
+    sd, ld = dev(s), dev(l)
+    surv = empty(n, k * S)
+    out = empty(n, e * S)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        codec.set_stream(st)
+        codec.fill_blocks(SEED, 0, n, B, k, S, d)
+        codec.encode(k, m, d, p)                      # warm-up: table cache, scratch
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        codec.rebuild(k, m, sd, surv, ld, out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        cs = torch.cuda.current_stream()
+        codec.set_stream(cs)
+        codec.encode(k, m, d, p)
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        codec.rebuild(k, m, sd, surv, ld, out)
+    codec.set_stream(None)
+    for fb in [100, 200]:
+        codec.fill_blocks(SEED, fb, n, B, k, S, d)
+        codec.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        data = O.fill_blocks(SEED, fb, n, B, k, S)
+        want = O.encode(k, m, S, data)
+        assert np.array_equal(host(p), want)
+        assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
+
+
+def test_concurrent_contexts_from_threads(O):
+    """One context per thread, all encoding at once (memo's background pool,
+    elle/src/elle/reactor/scheduler.cc:562-602): contexts are independent."""
+    import threading
+    import torch
+    from memo_amd import ec
+    k, m, B, n = 10, 4, 65536, 64
+    S = O.shard_size(B, k)
+    errs, results = [], {}
+
+    def work(t):
+        try:
+            with ec.Codec(0) as c:
+                d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+                p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+                for it in range(5):
+                    c.fill_blocks(SEED, 1000 * t + it, n, B, k, S, d)
+                    c.encode(k, m, d, p)
+                c.synchronize()
+                results[t] = host(p)
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(6)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
+    for t in range(6):
+        data = O.fill_blocks(SEED, 1000 * t + 4, n, B, k, S)
+        assert np.array_equal(results[t], O.encode(k, m, S, data))
