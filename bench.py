@@ -268,22 +268,28 @@ def main():
         del surv, out, want
 
     if not args.no_e2e and world == 1:
+        # PCIe-inclusive: blocks start and end in host memory (RPC socket in,
+        # silos/peers out).  3-stage pipeline, 64 MiB batches; never `value`.
         ne = min(n, 1024)
         hd = torch.empty((ne, k * S), dtype=torch.uint8).pin_memory()
         hp = torch.empty((ne, m * S), dtype=torch.uint8).pin_memory()
         hd.copy_(data[:ne].cpu())
         codec.set_stream(None)
-        codec.encode(k, m, hd, hp)
-        t = time.perf_counter()
-        reps = 3
-        for _ in range(reps):
-            codec.encode(k, m, hd, hp)
-        el = time.perf_counter() - t
-        ok = bool(torch.equal(hp[:4].cuda(), par[:4]))
+        e2e = {}
+        for kind, (src, dst) in [("pinned", (hd, hp)),
+                                 ("pageable", (hd.numpy().copy(), np.zeros((ne, m * S), np.uint8)))]:
+            codec.encode(k, m, src, dst)
+            t = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                codec.encode(k, m, src, dst)
+            el = time.perf_counter() - t
+            ok = bool(np.array_equal(np.asarray(dst[:4]), par[:4].cpu().numpy()))
+            e2e[kind] = {"value": round(reps * ne * B / el / 2**30, 3), "bit_exact": ok}
         result["end_to_end"] = {
-            "workload": "RS(%d,%d) encode, %d x %d-byte blocks from pinned host memory, parity back "
-                        "to pinned host (HtoD+kernel+DtoH, 2-stream pipeline)" % (k, m, ne, B),
-            "value": round(reps * ne * B / el / 2**30, 3), "unit": "GiB/s", "bit_exact": ok}
+            "workload": "RS(%d,%d) encode, %d x %d-byte blocks from host memory, parity back to "
+                        "host memory (HtoD + kernel + DtoH, 3-stage stream pipeline)" % (k, m, ne, B),
+            "unit": "GiB/s", "pinned": e2e["pinned"], "pageable": e2e["pageable"]}
         codec.set_stream(stream)
 
     if rank == 0 and world == 1 and not args.no_cpu:

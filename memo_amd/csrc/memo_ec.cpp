@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/memo_ec.h"
@@ -24,7 +25,10 @@ struct memo_ec_ctx {
   int device = 0;
   hipStream_t own = nullptr;      // ctx stream
   hipStream_t stream = nullptr;   // stream MEMO_EC_DEVICE work goes to
-  hipStream_t aux[2] = {nullptr, nullptr};  // host-pipeline streams
+  // host pipeline: copy-in / compute / copy-out streams, a ring of kSlots
+  // batch slots, and per-slot events chaining the three stages
+  hipStream_t sh = nullptr, sk = nullptr, sd = nullptr;
+  hipEvent_t ev_h[3] = {}, ev_k[3] = {}, ev_d[3] = {};
   uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
   uint32_t* d_tabs = nullptr;     // per-block product-table images (rebuild)
   size_t tabs_cap = 0;            // bytes
@@ -34,17 +38,17 @@ struct memo_ec_ctx {
   };
   std::vector<TabEntry> enc_tabs;  // cached encode images per (k, m, R, kpad)
   // host pipeline: device slots and pinned bounce buffers
-  uint8_t* d_slot[2] = {nullptr, nullptr};
+  uint8_t* d_slot[3] = {nullptr, nullptr, nullptr};
   size_t slot_cap = 0;
-  uint8_t* h_slot[2] = {nullptr, nullptr};
+  uint8_t* h_slot[3] = {nullptr, nullptr, nullptr};
   size_t hslot_cap = 0;
   int deferred = 0;
+  size_t pipe_bytes = 64ull << 20;  // host pipeline batch (MEMO_EC_PIPE_MB)
 };
 
 namespace {
 
 constexpr size_t kLdsBudget = 48 * 1024;  // table LDS per workgroup (flat mapping)
-constexpr size_t kPipeBytes = 64ull << 20;  // host pipeline batch (input bytes)
 
 int hip_rc(hipError_t e) {
   if (e == hipSuccess) return MEMO_EC_OK;
@@ -185,9 +189,38 @@ int ensure_tabs(memo_ec_ctx* ctx, size_t bytes) {
   return MEMO_EC_OK;
 }
 
+constexpr int kSlots = 3;
+
+// Pageable <-> pinned bounce copies run on several host threads: one thread
+// moves ~10-20 GB/s, below the ~50 GB/s a PCIe Gen5 x16 direction carries.
+void par_memcpy(void* dst, const void* src, size_t n) {
+  constexpr size_t kMin = 8u << 20;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>({8, hw, n / kMin});
+  if (nt <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  std::vector<std::thread> ts;
+  const size_t per = (n / nt + 63) & ~(size_t)63;
+  for (size_t t = 1; t < nt; ++t) {
+    const size_t lo = t * per;
+    if (lo >= n) break;
+    const size_t len = std::min(per, n - lo);
+    ts.emplace_back([=] { std::memcpy((char*)dst + lo, (const char*)src + lo, len); });
+  }
+  std::memcpy(dst, src, std::min(per, n));
+  for (auto& th : ts) th.join();
+}
+
+int sync_pipeline(memo_ec_ctx* ctx) {
+  for (auto st : {ctx->sh, ctx->sk, ctx->sd}) HIPCHK(hipStreamSynchronize(st));
+  return MEMO_EC_OK;
+}
+
 int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
   if (dev_bytes > ctx->slot_cap) {
-    for (auto& st : ctx->aux) HIPCHK(hipStreamSynchronize(st));
+    if (int rc = sync_pipeline(ctx)) return rc;
     for (auto& p : ctx->d_slot) {
       if (p) HIPCHK(hipFree(p));
       p = nullptr;
@@ -196,7 +229,7 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
     ctx->slot_cap = dev_bytes;
   }
   if (host_bytes > ctx->hslot_cap) {
-    for (auto& st : ctx->aux) HIPCHK(hipStreamSynchronize(st));
+    if (int rc = sync_pipeline(ctx)) return rc;
     for (auto& p : ctx->h_slot) {
       if (p) HIPCHK(hipHostFree(p));
       p = nullptr;
@@ -257,6 +290,43 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
 size_t tab_bytes(int k, int e, size_t n) {
   const int KC = mac_kchunk(k), R = mac_rbound(e);
   return n * (size_t)R * kpad_of((uint32_t)k, KC) * 32;
+}
+
+// Host-memory pipeline over batches of nb blocks.  Batch i uses slot i % 3:
+//   in(slot, b0, cnt)       host staging + HtoD copies on sh
+//   run(slot, b0, cnt, sk)  kernels on sk, after the slot's HtoD (event)
+//   out(slot, b0, cnt)      DtoH copies on sd, after the kernels (event)
+//   done(slot, b0, cnt)     host side after the DtoH (pageable copy-out)
+// so the HtoD of batch i+1 runs under the DtoH of batch i (PCIe duplex).
+template <class In, class Run, class Out, class Done>
+int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, Done done) {
+  size_t off[kSlots] = {}, cnt[kSlots] = {};
+  const size_t nbatch = (n + nb - 1) / nb;
+  auto finish = [&](int s) -> int {
+    if (!cnt[s]) return MEMO_EC_OK;
+    HIPCHK(hipEventSynchronize(c->ev_d[s]));
+    done(s, off[s], cnt[s]);
+    cnt[s] = 0;
+    return MEMO_EC_OK;
+  };
+  for (size_t bi = 0; bi < nbatch; ++bi) {
+    const int s = (int)(bi % kSlots);
+    if (int rc = finish(s)) return rc;
+    const size_t b0 = bi * nb, cn = std::min(nb, n - b0);
+    if (int rc = in(s, b0, cn)) return rc;
+    HIPCHK(hipEventRecord(c->ev_h[s], c->sh));
+    HIPCHK(hipStreamWaitEvent(c->sk, c->ev_h[s], 0));
+    if (int rc = run(s, b0, cn, c->sk)) return rc;
+    HIPCHK(hipEventRecord(c->ev_k[s], c->sk));
+    HIPCHK(hipStreamWaitEvent(c->sd, c->ev_k[s], 0));
+    if (int rc = out(s, b0, cn)) return rc;
+    HIPCHK(hipEventRecord(c->ev_d[s], c->sd));
+    off[s] = b0;
+    cnt[s] = cn;
+  }
+  for (size_t bi = nbatch > kSlots ? nbatch - kSlots : 0; bi < nbatch; ++bi)
+    if (int rc = finish((int)(bi % kSlots))) return rc;
+  return MEMO_EC_OK;
 }
 
 int take_deferred(memo_ec_ctx* ctx) {
@@ -322,12 +392,25 @@ int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
   c->device = device;
   int rc = MEMO_EC_OK;
   if ((rc = hip_rc(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking))) ||
-      (rc = hip_rc(hipStreamCreateWithFlags(&c->aux[0], hipStreamNonBlocking))) ||
-      (rc = hip_rc(hipStreamCreateWithFlags(&c->aux[1], hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipStreamCreateWithFlags(&c->sh, hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipStreamCreateWithFlags(&c->sk, hipStreamNonBlocking))) ||
+      (rc = hip_rc(hipStreamCreateWithFlags(&c->sd, hipStreamNonBlocking))) ||
       (rc = hip_rc(hipMalloc(&c->d_status, 256))) ||
       (rc = hip_rc(hipMemset(c->d_status, 0, 256)))) {
     memo_ec_ctx_destroy(c);
     return rc;
+  }
+  for (int i = 0; i < kSlots; ++i) {
+    if ((rc = hip_rc(hipEventCreateWithFlags(&c->ev_h[i], hipEventDisableTiming))) ||
+        (rc = hip_rc(hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming))) ||
+        (rc = hip_rc(hipEventCreateWithFlags(&c->ev_d[i], hipEventDisableTiming)))) {
+      memo_ec_ctx_destroy(c);
+      return rc;
+    }
+  }
+  if (const char* p = std::getenv("MEMO_EC_PIPE_MB")) {
+    const long v = std::atol(p);
+    if (v >= 1 && v <= 4096) c->pipe_bytes = (size_t)v << 20;
   }
   c->stream = c->own;
   *out = c;
@@ -339,7 +422,7 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
   DeviceGuard g(c->device);
   if (c->own) (void)hipStreamSynchronize(c->own);
   if (c->stream && c->stream != c->own) (void)hipStreamSynchronize(c->stream);
-  for (auto& st : c->aux)
+  for (auto st : {c->sh, c->sk, c->sd})
     if (st) (void)hipStreamSynchronize(st);
   for (auto& p : c->d_slot)
     if (p) (void)hipFree(p);
@@ -348,7 +431,10 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
   if (c->d_tabs) (void)hipFree(c->d_tabs);
   for (auto& e : c->enc_tabs) (void)hipFree(e.dev);
   if (c->d_status) (void)hipFree(c->d_status);
-  for (auto& st : c->aux)
+  for (int i = 0; i < kSlots; ++i)
+    for (auto ev : {c->ev_h[i], c->ev_k[i], c->ev_d[i]})
+      if (ev) (void)hipEventDestroy(ev);
+  for (auto st : {c->sh, c->sk, c->sd})
     if (st) (void)hipStreamDestroy(st);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
@@ -380,45 +466,33 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   if (where == MEMO_EC_DEVICE) return encode_device(c, k, m, S, n, data, parity, c->stream);
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
-  // Host pipeline: batches of nb blocks alternate between two slots/streams;
-  // batch i+1's copy-in overlaps batch i's kernel and copy-out.
   const size_t in_b = (size_t)k * S, out_b = (size_t)m * S;
-  size_t nb = std::max<size_t>(1, kPipeBytes / in_b);
+  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
   nb = std::min(nb, n);
   const bool pinned = where == MEMO_EC_HOST_PINNED;
   if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
-  const size_t nbatch = (n + nb - 1) / nb;
-  std::vector<size_t> pend_off(2, 0), pend_cnt(2, 0);
-  auto drain = [&](int s) -> int {
-    if (!pend_cnt[s]) return MEMO_EC_OK;
-    HIPCHK(hipStreamSynchronize(c->aux[s]));
-    if (!pinned)
-      std::memcpy(parity + pend_off[s] * out_b, c->h_slot[s] + pend_cnt[s] * in_b,
-                  pend_cnt[s] * out_b);
-    pend_cnt[s] = 0;
-    return MEMO_EC_OK;
-  };
-  for (size_t bi = 0; bi < nbatch; ++bi) {
-    const int s = (int)(bi & 1);
-    if (int rc = drain(s)) return rc;
-    const size_t b0 = bi * nb, cnt = std::min(nb, n - b0);
-    uint8_t* din = c->d_slot[s];
-    uint8_t* dout = din + cnt * in_b;
-    const uint8_t* src = data + b0 * in_b;
-    if (!pinned) {
-      std::memcpy(c->h_slot[s], src, cnt * in_b);
-      src = c->h_slot[s];
-    }
-    HIPCHK(hipMemcpyAsync(din, src, cnt * in_b, hipMemcpyHostToDevice, c->aux[s]));
-    if (int rc = encode_device(c, k, m, S, cnt, din, dout, c->aux[s])) return rc;
-    uint8_t* dst = pinned ? parity + b0 * out_b : c->h_slot[s] + cnt * in_b;
-    HIPCHK(hipMemcpyAsync(dst, dout, cnt * out_b, hipMemcpyDeviceToHost, c->aux[s]));
-    pend_off[s] = b0;
-    pend_cnt[s] = cnt;
-  }
-  for (int s = 0; s < 2; ++s)
-    if (int rc = drain(s)) return rc;
-  return MEMO_EC_OK;
+  // slot layout (device and pageable bounce): [data nb*in_b | parity nb*out_b]
+  return run_pipeline(
+      c, n, nb,
+      [&](int s, size_t b0, size_t cnt) -> int {
+        const uint8_t* src = data + b0 * in_b;
+        if (!pinned) {
+          par_memcpy(c->h_slot[s], src, cnt * in_b);
+          src = c->h_slot[s];
+        }
+        return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, c->sh));
+      },
+      [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
+        return encode_device(c, k, m, S, cnt, c->d_slot[s], c->d_slot[s] + nb * in_b, st);
+      },
+      [&](int s, size_t b0, size_t cnt) -> int {
+        uint8_t* dst = pinned ? parity + b0 * out_b : c->h_slot[s] + nb * in_b;
+        return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + nb * in_b, cnt * out_b,
+                                     hipMemcpyDeviceToHost, c->sd));
+      },
+      [&](int s, size_t b0, size_t cnt) {
+        if (!pinned) par_memcpy(parity + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
+      });
 }
 
 int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* surv_idx,
@@ -452,55 +526,44 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
 
   const size_t in_b = (size_t)k * S, out_b = (size_t)e * S;
   const size_t idx_b = (size_t)k + e;
-  size_t nb = std::max<size_t>(1, kPipeBytes / in_b);
+  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
   nb = std::min(nb, n);
   const bool pinned = where == MEMO_EC_HOST_PINNED;
-  // slot layout: [surv | out | surv_idx | lost_idx], host bounce likewise
+  // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e]
   const size_t slot = nb * (in_b + out_b + idx_b);
   if (int rc = ensure_slots(c, slot, slot)) return rc;
-  if (int rc = ensure_tabs(c, 2 * tab_bytes(k, e, nb))) return rc;
-  const size_t nbatch = (n + nb - 1) / nb;
-  std::vector<size_t> pend_off(2, 0), pend_cnt(2, 0);
-  auto drain = [&](int s) -> int {
-    if (!pend_cnt[s]) return MEMO_EC_OK;
-    HIPCHK(hipStreamSynchronize(c->aux[s]));
-    if (!pinned)
-      std::memcpy(out + pend_off[s] * out_b, c->h_slot[s] + pend_cnt[s] * in_b,
-                  pend_cnt[s] * out_b);
-    pend_cnt[s] = 0;
-    return MEMO_EC_OK;
-  };
-  for (size_t bi = 0; bi < nbatch; ++bi) {
-    const int s = (int)(bi & 1);
-    if (int rc = drain(s)) return rc;
-    const size_t b0 = bi * nb, cnt = std::min(nb, n - b0);
-    uint8_t* dsurv = c->d_slot[s];
-    uint8_t* dout = dsurv + cnt * in_b;
-    uint8_t* dsidx = dout + cnt * out_b;
-    uint8_t* dlidx = dsidx + cnt * k;
-    uint8_t* h = c->h_slot[s];
-    // indices always go through the pinned slot (small)
-    std::memcpy(h + cnt * (in_b + out_b), surv_idx + b0 * k, cnt * k);
-    std::memcpy(h + cnt * (in_b + out_b) + cnt * k, lost_idx + b0 * e, cnt * e);
-    HIPCHK(hipMemcpyAsync(dsidx, h + cnt * (in_b + out_b), cnt * idx_b, hipMemcpyHostToDevice,
-                          c->aux[s]));
-    const uint8_t* src = surv + b0 * in_b;
-    if (!pinned) {
-      std::memcpy(h, src, cnt * in_b);
-      src = h;
-    }
-    HIPCHK(hipMemcpyAsync(dsurv, src, cnt * in_b, hipMemcpyHostToDevice, c->aux[s]));
-    uint32_t* tabs = c->d_tabs + (size_t)s * tab_bytes(k, e, nb) / 4;
-    if (int rc = rebuild_device(c, k, m, S, cnt, dsidx, dsurv, dlidx, e, dout, nullptr, tabs,
-                                c->aux[s]))
-      return rc;
-    uint8_t* dst = pinned ? out + b0 * out_b : h + cnt * in_b;
-    HIPCHK(hipMemcpyAsync(dst, dout, cnt * out_b, hipMemcpyDeviceToHost, c->aux[s]));
-    pend_off[s] = b0;
-    pend_cnt[s] = cnt;
-  }
-  for (int s = 0; s < 2; ++s)
-    if (int rc = drain(s)) return rc;
+  const size_t tabs = tab_bytes(k, e, nb);
+  if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
+  const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
+  const int rc = run_pipeline(
+      c, n, nb,
+      [&](int s, size_t b0, size_t cnt) -> int {
+        uint8_t* h = c->h_slot[s];
+        uint8_t* d = c->d_slot[s];
+        std::memcpy(h + o_sidx, surv_idx + b0 * k, cnt * k);  // indices: always bounced
+        std::memcpy(h + o_lidx, lost_idx + b0 * e, cnt * e);
+        HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx, nb * idx_b, hipMemcpyHostToDevice, c->sh));
+        const uint8_t* src = surv + b0 * in_b;
+        if (!pinned) {
+          par_memcpy(h, src, cnt * in_b);
+          src = h;
+        }
+        return hip_rc(hipMemcpyAsync(d, src, cnt * in_b, hipMemcpyHostToDevice, c->sh));
+      },
+      [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
+        uint8_t* d = c->d_slot[s];
+        return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out, nullptr,
+                              c->d_tabs + (size_t)s * tabs / 4, st);
+      },
+      [&](int s, size_t b0, size_t cnt) -> int {
+        uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + o_out;
+        return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + o_out, cnt * out_b, hipMemcpyDeviceToHost,
+                                     c->sd));
+      },
+      [&](int s, size_t b0, size_t cnt) {
+        if (!pinned) par_memcpy(out + b0 * out_b, c->h_slot[s] + o_out, cnt * out_b);
+      });
+  if (rc) return rc;
   return take_deferred(c);
 }
 
