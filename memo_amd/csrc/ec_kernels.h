@@ -18,6 +18,10 @@
 #ifndef MEMO_EC_MAC_XCD
 #define MEMO_EC_MAC_XCD 1
 #endif
+// 1: always use the LDS Gauss-Jordan kernel (the register one serves k <= 32)
+#ifndef MEMO_EC_DECODE_LDS
+#define MEMO_EC_DECODE_LDS 0
+#endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif

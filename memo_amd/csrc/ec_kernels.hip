@@ -476,6 +476,122 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
   }
 }
 
+// Register-resident variant for k <= K (K in {4, 8, 16, 32}): lane l holds
+// column l of the K x 2K matrix [A | I] in VGPRs (A padded to K x K with an
+// identity block, whose inverse is the identity, so rows/columns >= k never
+// mix with the real ones).  Pivot rows and row factors are broadcast with
+// v_readlane; each elimination is one independent log/antilog LDS lookup per
+// row and lane (no LDS round trip of the matrix, no wave barriers).
+template <int K>
+__global__ void __launch_bounds__(256) decode_rows_reg_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  uint32_t* s_gf = smem;
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
+  const uint8_t* ex = lg + 256;
+  stage_gf(s_gf);
+  __syncthreads();
+
+  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const uint64_t b = (uint64_t)blockIdx.x * 4 + wave;
+  if (b >= a.n) return;
+  const uint32_t k = a.k, e = a.e, total = a.k + a.m;
+  uint8_t* Rw = reinterpret_cast<uint8_t*>(smem + 192) + wave * (MEMO_EC_MAX_M * MEMO_EC_MAX_K);
+  const uint8_t* sidx = a.surv_idx + b * k;
+  const uint8_t* lidx = a.lost_idx + b * e;
+
+  const bool left = lane < K;
+  const uint32_t col = left ? lane : lane - K;  // lanes >= 2K carry copies, unused
+  uint32_t m[K];
+  bool bad = false;
+#pragma unroll
+  for (int r = 0; r < K; ++r) {
+    if ((uint32_t)r < k) {
+      const uint32_t sv = sidx[r];
+      bad |= sv >= total;
+      if (left) m[r] = (col < k && sv < total) ? gen_entry(lg, ex, k, sv, col) : 0u;
+      else m[r] = col == (uint32_t)r ? 1u : 0u;
+    } else {
+      m[r] = col == (uint32_t)r ? 1u : 0u;  // identity padding, both halves
+    }
+  }
+
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    if (bad) break;
+    // pivot: first row >= c with a nonzero entry in column c (lane c)
+    uint32_t pl = K;
+#pragma unroll
+    for (int r = K - 1; r >= c; --r)
+      if (m[r]) pl = r;
+    const uint32_t p = __builtin_amdgcn_readlane(pl, c);
+    if (p >= (uint32_t)K) {
+      bad = true;
+      break;
+    }
+    if (p != (uint32_t)c) {
+#pragma unroll
+      for (int r = c + 1; r < K; ++r)
+        if (p == (uint32_t)r) {
+          const uint32_t t = m[c];
+          m[c] = m[r];
+          m[r] = t;
+        }
+    }
+    const uint32_t piv = __builtin_amdgcn_readlane(m[c], c);
+    const uint32_t ilog = 255u - lg[piv];  // log of the pivot's inverse
+    const bool nz = m[c] != 0;
+    uint32_t lc = lg[m[c]] + ilog;          // log of the normalised entry
+    if (lc >= 255) lc -= 255;
+    m[c] = nz ? (uint32_t)ex[lc] : 0u;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+      if (r == c) continue;
+      const uint32_t f = __builtin_amdgcn_readlane(m[r], c);
+      if (f) m[r] ^= nz ? (uint32_t)ex[lc + lg[f]] : 0u;
+    }
+  }
+
+  // Right half, lane K+j, now holds column j of A^-1: inv[t][j] = m[t].
+  for (uint32_t r = 0; r < e; ++r) {
+    const uint32_t l = lidx[r];
+    const bool lbad = bad || l >= total;
+    if (!left && col < k) {
+      uint32_t acc = 0;
+      if (!lbad) {
+        if (l < k) {
+#pragma unroll
+          for (int t = 0; t < K; ++t)
+            if ((uint32_t)t == l) acc = m[t];
+        } else {
+#pragma unroll
+          for (int t = 0; t < K; ++t)
+            if ((uint32_t)t < k) acc ^= gf_mul_t(lg, ex, gf_inv_t(lg, ex, l ^ (uint32_t)t), m[t]);
+        }
+      }
+      Rw[r * k + col] = (uint8_t)acc;
+    }
+    if (lbad) bad = true;
+  }
+  wave_sync();
+  if (bad) {
+    for (uint32_t t = lane; t < e * k; t += 64) Rw[t] = 0;
+    wave_sync();
+    if (lane == 0 && a.status) atomicOr(a.status, 1u);
+  }
+  if (a.rows)
+    for (uint32_t t = lane; t < e * k; t += 64) a.rows[b * (uint64_t)e * k + t] = Rw[t];
+  if (a.tab) {
+    uint32_t* dst = a.tab + b * (uint64_t)a.R * a.kpad * 8;
+    const uint32_t n = a.R * a.kpad * 8;
+    for (uint32_t t = lane; t < n; t += 64) {
+      const uint32_t q = t & 7, cidx = t >> 3;
+      const uint32_t i = cidx / a.kpad, j = cidx - i * a.kpad;
+      const uint32_t c = (i < e && j < k) ? Rw[i * k + j] : 0u;
+      dst[t] = table_dword(lg, ex, c, q);
+    }
+  }
+}
+
 // ------------------------------------------------------------- synthetic fill
 __device__ __forceinline__ uint64_t sm64_mix(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -583,9 +699,20 @@ hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t l
 hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st) {
   const uint32_t grid = (uint32_t)((a.n + 3) / 4);
   if (grid == 0) return hipSuccess;
-  const size_t lds = 768 + 4 * (size_t)MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K +
-                     4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
-  hipLaunchKernelGGL(decode_rows_kernel, dim3(grid), dim3(256), lds, st, a);
+  const size_t lds_reg = 768 + 4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
+  if (a.k <= 4 && !MEMO_EC_DECODE_LDS) {
+    hipLaunchKernelGGL(decode_rows_reg_kernel<4>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else if (a.k <= 8 && !MEMO_EC_DECODE_LDS) {
+    hipLaunchKernelGGL(decode_rows_reg_kernel<8>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else if (a.k <= 16 && !MEMO_EC_DECODE_LDS) {
+    hipLaunchKernelGGL(decode_rows_reg_kernel<16>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else if (a.k <= 32 && !MEMO_EC_DECODE_LDS) {
+    hipLaunchKernelGGL(decode_rows_reg_kernel<32>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else {
+    const size_t lds = 768 + 4 * (size_t)MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K +
+                       4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
+    hipLaunchKernelGGL(decode_rows_kernel, dim3(grid), dim3(256), lds, st, a);
+  }
   return hipGetLastError();
 }
 
