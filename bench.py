@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sweep", action="store_true", help="also run the C5 mixed sweep")
+    ap.add_argument("--sha", action="store_true",
+                    help="also time GPU SHA-256 (CHB addresses) of the batch and of 4 KiB blocks")
     ap.add_argument("--sweep-gib", type=float, default=4.0, help="payload GiB per sweep point")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
@@ -295,6 +297,35 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = par[:4].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, sample)
+
+    if args.sha and world == 1:
+        import hashlib
+        res = {}
+        for name, nb, bb in [("C2 batch, 1 MiB blocks", n, B), ("4 KiB blocks", 1 << 20, 4096)]:
+            msg = data if bb == B else torch.empty((nb, bb), dtype=torch.uint8, device="cuda")
+            stride = msg.shape[1]
+            if bb != B:
+                codec.fill_blocks(SEED, 0, nb, bb, 1, bb, msg)
+            pre = torch.zeros((nb, 64), dtype=torch.uint8, device="cuda")  # salt || owner
+            dig = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
+            fn = lambda: codec.sha256(msg, dig, prefix=pre, uniform_len=bb, msg_stride=stride)  # noqa
+            _, kms = timed_launches(torch, fn, 5, 1, None, stream)
+            ms = float(np.mean(kms))
+            ok = dig[0].cpu().numpy().tobytes() == hashlib.sha256(
+                bytes(64) + msg[0, :bb].cpu().numpy().tobytes()).digest()
+            one = msg[0, :bb].cpu().numpy().tobytes()
+            t = time.perf_counter()
+            reps = max(1, (64 << 20) // bb)
+            for _ in range(reps):
+                hashlib.sha256(one).digest()
+            cpu = reps * bb / (time.perf_counter() - t) / 1e9
+            res[name] = {"blocks": nb, "block_bytes": bb, "kernel_ms": round(ms, 3),
+                         "GBs": round(nb * (bb + 64) / (ms * 1e-3) / 1e9, 1), "bit_exact": ok,
+                         "cpu_1core_GBs": round(cpu, 2)}
+            if bb != B:
+                del msg
+        result["sha256"] = {"workload": "batched SHA-256(salt||owner||data) = CHB addresses "
+                                        "(CHB.cc:264-289), one lane per block", **res}
 
     if args.sweep and world == 1:
         del data, par

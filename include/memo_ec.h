@@ -131,6 +131,21 @@ int memo_ec_decode_rows(memo_ec_ctx *ctx, int k, int m, size_t n,
 int memo_ec_encode_segments(memo_ec_ctx *ctx, int nseg,
                             const memo_ec_segment *segs);
 
+/* Batched SHA-256 (FIPS 180-4): digest_i = SHA-256(prefix_i || msg_i) for
+ * i < n, with prefix_i = prefix + i*prefix_stride (prefix_len bytes; 0 for
+ * none) and msg_i = msg + i*msg_stride of msg_len[i] bytes (msg_len == NULL:
+ * uniform_len for all).  digest: n x 32 bytes.  This is the CHB address hash
+ * SHA-256(salt || owner || data) of CHB::_hash_address
+ * (src/memo/model/doughnut/CHB.cc:264-289) and of CHB::_validate
+ * (CHB.cc:79-99) for a whole batch; the caller sets address byte 31 to the
+ * immutable flag (model/Address.hh: flag_byte).  Device pointers only;
+ * asynchronous on the ctx stream. */
+int memo_ec_sha256_batch(memo_ec_ctx *ctx, size_t n, const uint8_t *prefix,
+                         size_t prefix_len, size_t prefix_stride,
+                         const uint8_t *msg, size_t msg_stride,
+                         const uint64_t *msg_len, size_t uniform_len,
+                         uint8_t *digest);
+
 /* Synthetic workload helpers (device memory; asynchronous on the ctx
  * stream).  Bytes and erasure patterns follow DESIGN.md section 6. */
 int memo_ec_fill_blocks(memo_ec_ctx *ctx, uint64_t seed, uint64_t first_block,

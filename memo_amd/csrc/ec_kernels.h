@@ -22,6 +22,9 @@
 #ifndef MEMO_EC_DECODE_LDS
 #define MEMO_EC_DECODE_LDS 0
 #endif
+#ifndef MEMO_EC_MAC_WOUTER
+#define MEMO_EC_MAC_WOUTER 0
+#endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif
@@ -70,6 +73,14 @@ struct DecodeArgs {
   uint32_t k, m, e, R, kpad;
 };
 
+struct Sha256Args {
+  const uint8_t* prefix;  // message i = prefix + i*prefix_stride (prefix_len B) || msg_i
+  const uint8_t* msg;     // msg_i = msg + i*msg_stride, msg_len[i] (or uniform_len) bytes
+  const uint64_t* msg_len;
+  uint8_t* digest;        // n x 32
+  uint64_t n, prefix_len, prefix_stride, msg_stride, uniform_len;
+};
+
 struct FillArgs {
   uint8_t* out;
   uint64_t seed, first_block, n, B, stride;
@@ -94,6 +105,7 @@ hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t l
                       hipStream_t st);
 hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st);
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);
+hipError_t launch_sha256(const Sha256Args& a, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);
 const uint8_t* host_gf_log();
 const uint8_t* host_gf_exp();

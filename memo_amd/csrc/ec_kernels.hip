@@ -161,6 +161,45 @@ __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl
 template <int KC, int R>
 __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
                                           const uint32_t* tab, uint32_t kpad, uint32_t j0) {
+#if MEMO_EC_MAC_WOUTER
+  // dword-outer order: 6 selector registers live instead of 24; the
+  // broadcast tables are re-read from LDS per dword (an opaque offset keeps
+  // the compiler from caching all R pairs of tables in registers).
+#pragma unroll
+  for (int g = 0; g < KC; g += 2) {
+    const bool two = g + 1 < KC;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t xa = w == 0 ? d[g].x : w == 1 ? d[g].y : w == 2 ? d[g].z : d[g].w;
+      const Sel sa = make_sel(xa);
+      Sel sb{};
+      if (two) {
+        const uint32_t xb = w == 0 ? d[g + 1].x : w == 1 ? d[g + 1].y : w == 2 ? d[g + 1].z : d[g + 1].w;
+        sb = make_sel(xb);
+      }
+      uint32_t off = (j0 + g) * 8;
+      asm volatile("" : "+v"(off));
+#pragma unroll
+      for (int i = 0; i < R; ++i) {
+        const uint32_t* tp = tab + off + i * kpad * 8;
+        const Tab ta = read_tab(tp);
+        uint32_t al, am, ah;
+        lookups(sa, ta, al, am, ah);
+        if (two) {
+          const Tab tb = read_tab(tp + 8);
+          uint32_t bl, bm, bh;
+          lookups(sb, tb, bl, bm, bh);
+          const uint32_t x = xor3(acc[i][w], al, am);
+          const uint32_t y = xor3(ah, bl, bm);
+          acc[i][w] = xor3(x, y, bh);
+        } else {
+          acc[i][w] = xor3(acc[i][w], al, am) ^ ah;
+        }
+      }
+    }
+  }
+  return;
+#endif
 #pragma unroll
   for (int g = 0; g < KC; g += MAC_PAIR ? 2 : 1) {
     const bool two = MAC_PAIR && g + 1 < KC;
@@ -647,6 +686,123 @@ __global__ void __launch_bounds__(256) gather_kernel(GatherArgs a) {
     }
     *reinterpret_cast<uint4*>(a.out + br * a.S + off) = v;
   }
+}
+
+// ------------------------------------------------------------- SHA-256
+// Batched SHA-256 (FIPS 180-4) of n messages prefix_b || msg_b: the CHB
+// address hash SHA-256(salt || owner || data) of CHB::_hash_address
+// (src/memo/model/doughnut/CHB.cc:264-289) for a whole batch of blocks.  One
+// lane per message (SHA-256 is sequential within a message); interior
+// 64-byte chunks are read with 4 dwordx4 loads, edge chunks byte-wise.
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
+
+// One SHA-256 compression.  Sigma/sigma are 3-input XORs and Ch/Maj single
+// v_bitop3_b32 truth tables (0xCA, 0xE8), sums v_add3_u32: a short
+// dependency chain per round, which bounds large blocks (one lane each).
+__device__ __forceinline__ void sha256_compress(uint32_t (&h)[8], uint32_t (&w)[16]) {
+  uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+#pragma unroll
+  for (int t = 0; t < 64; ++t) {
+    uint32_t wt;
+    if (t < 16) {
+      wt = w[t];
+    } else {
+      const uint32_t w15 = w[(t + 1) & 15], w2 = w[(t + 14) & 15];
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
+      wt = w[t & 15] + s0 + w[(t + 9) & 15] + s1;
+      w[t & 15] = wt;
+    }
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
+    const uint32_t ch = __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+    const uint32_t t1 = hh + S1 + ch + (kSha256K[t] + wt);
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
+    const uint32_t mj = __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+    hh = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + S0 + mj;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+
+// Byte o of the padded virtual message prefix || body || 0x80 0.. || len64.
+__device__ __forceinline__ uint32_t sha_byte(const uint8_t* pre, uint64_t P, const uint8_t* body,
+                                             uint64_t L, uint64_t total_bits, uint64_t padded,
+                                             uint64_t o) {
+  if (o < P) return pre[o];
+  if (o < P + L) return body[o - P];
+  if (o == P + L) return 0x80;
+  if (o >= padded - 8) return (uint32_t)(total_bits >> (8 * (padded - 1 - o))) & 0xff;
+  return 0;
+}
+
+__global__ void __launch_bounds__(256) sha256_kernel(Sha256Args a) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint8_t* pre = a.prefix + i * a.prefix_stride;
+  const uint8_t* body = a.msg + i * a.msg_stride;
+  const uint64_t P = a.prefix_len;
+  const uint64_t L = a.msg_len ? a.msg_len[i] : a.uniform_len;
+  const uint64_t total = P + L;
+  const uint64_t padded = (total + 9 + 63) / 64 * 64;
+  const uint64_t bits = total * 8;
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  // body chunks [c_lo, c_hi) are whole 64-byte chunks inside the body whose
+  // body offset is 16-byte aligned (fast path)
+  const bool fast = (P % 16) == 0 && (((uintptr_t)body) % 16) == 0;
+  const uint64_t c_lo = (P + 63) / 64;
+  const uint64_t c_hi = (P + L) / 64;
+  const uint64_t nchunks = padded / 64;
+  for (uint64_t c = 0; c < nchunks; ++c) {
+    uint32_t w[16];
+    if (fast && c >= c_lo && c < c_hi) {
+      const uint4* q = reinterpret_cast<const uint4*>(body + (c * 64 - P));
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + v));
+        w[4 * v + 0] = __builtin_bswap32(x.x);
+        w[4 * v + 1] = __builtin_bswap32(x.y);
+        w[4 * v + 2] = __builtin_bswap32(x.z);
+        w[4 * v + 3] = __builtin_bswap32(x.w);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) {
+        const uint64_t o = c * 64 + 4 * t;
+        w[t] = (sha_byte(pre, P, body, L, bits, padded, o) << 24) |
+               (sha_byte(pre, P, body, L, bits, padded, o + 1) << 16) |
+               (sha_byte(pre, P, body, L, bits, padded, o + 2) << 8) |
+               sha_byte(pre, P, body, L, bits, padded, o + 3);
+      }
+    }
+    sha256_compress(h, w);
+  }
+  uint32_t* out = reinterpret_cast<uint32_t*>(a.digest + i * 32);
+#pragma unroll
+  for (int t = 0; t < 8; ++t) out[t] = __builtin_bswap32(h[t]);
+}
+
+hipError_t launch_sha256(const Sha256Args& a, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  const uint64_t grid = (a.n + 255) / 256;
+  hipLaunchKernelGGL(sha256_kernel, dim3((uint32_t)grid), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------- launchers

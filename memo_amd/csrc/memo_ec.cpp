@@ -597,6 +597,17 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
   return launch_plans(plans, c->stream);
 }
 
+int memo_ec_sha256_batch(memo_ec_ctx* c, size_t n, const uint8_t* prefix, size_t prefix_len,
+                         size_t prefix_stride, const uint8_t* msg, size_t msg_stride,
+                         const uint64_t* msg_len, size_t uniform_len, uint8_t* digest) {
+  if (!c || (n && (!digest || !msg || (prefix_len && !prefix)))) return MEMO_EC_EINVAL;
+  if (n == 0) return MEMO_EC_OK;
+  if (n > 0x7fffffffull * 256) return MEMO_EC_ERANGE;
+  DeviceGuard g(c->device);
+  Sha256Args a{prefix, msg, msg_len, digest, n, prefix_len, prefix_stride, msg_stride, uniform_len};
+  return hip_rc(launch_sha256(a, c->stream));
+}
+
 int memo_ec_fill_blocks(memo_ec_ctx* c, uint64_t seed, uint64_t first_block, size_t n, size_t B,
                         int k, size_t S, uint8_t* out) {
   if (!c || k < 1 || S % 16 || (size_t)k * S < B || (n && !out)) return MEMO_EC_EINVAL;

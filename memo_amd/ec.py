@@ -47,7 +47,8 @@ EXPORTS = [
     "memo_ec_ctx_create", "memo_ec_ctx_destroy", "memo_ec_set_stream", "memo_ec_get_stream",
     "memo_ec_synchronize", "memo_ec_shard_size", "memo_ec_generator", "memo_ec_encode_batch",
     "memo_ec_rebuild_batch", "memo_ec_decode_rows", "memo_ec_encode_segments",
-    "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards", "memo_ec_strerror",
+    "memo_ec_sha256_batch", "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards",
+    "memo_ec_strerror",
     "memo_ec_version",
 ]
 
@@ -73,6 +74,8 @@ def _lib():
                                             _u8p, c_int, _u8p, c_int]
         L.memo_ec_decode_rows.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _u8p, _u8p, c_int, _u8p]
         L.memo_ec_encode_segments.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(Segment)]
+        L.memo_ec_sha256_batch.argtypes = [ctypes.c_void_p, _sz, _u8p, _sz, _sz, _u8p, _sz,
+                                           ctypes.c_void_p, _sz, _u8p]
         L.memo_ec_fill_blocks.argtypes = [ctypes.c_void_p, c_u64, c_u64, _sz, _sz, c_int, _sz, _u8p]
         L.memo_ec_erasures.argtypes = [c_u64, c_u64, _sz, c_int, c_int, c_int, _u8p, _u8p]
         L.memo_ec_gather_shards.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
@@ -222,6 +225,19 @@ class Codec:
         for i, (k, m, S, n, d, p) in enumerate(segs):
             arr[i] = Segment(k, m, S, n, _ptr(d)[0], _ptr(p)[0])
         _check(_lib().memo_ec_encode_segments(self._ctx, len(segs), arr), "encode_segments")
+
+    def sha256(self, msg, digest, prefix=None, msg_len=None, uniform_len=None, msg_stride=None):
+        """digest[i] = SHA-256(prefix[i] || msg[i]) on the GPU (CHB address hash).
+        msg: uint8 (n, stride) device tensor; msg_len: int64 device tensor or
+        None (uniform_len bytes, default the row length); prefix: (n, P) or None."""
+        n = msg.shape[0]
+        stride = msg_stride if msg_stride is not None else msg.shape[1]
+        pp, pl, ps = (0, 0, 0) if prefix is None else (_ptr(prefix)[0], prefix.shape[1], prefix.shape[1])
+        lp = 0 if msg_len is None else msg_len.data_ptr()
+        ul = stride if uniform_len is None else uniform_len
+        _check(_lib().memo_ec_sha256_batch(self._ctx, n, pp or None, pl, ps, _ptr(msg)[0], stride,
+                                           lp or None, ul, _ptr(digest)[0]), "sha256")
+        return digest
 
     def fill_blocks(self, seed, first_block, n, B, k, S, out):
         _check(_lib().memo_ec_fill_blocks(self._ctx, seed, first_block, n, B, k, S, _ptr(out)[0]),

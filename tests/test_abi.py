@@ -13,7 +13,7 @@ from conftest import ROOT, SEED
 
 def header_symbols():
     txt = open(os.path.join(ROOT, "include", "memo_ec.h")).read()
-    return sorted(set(re.findall(r"\b(memo_ec_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(memo_ec_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_and_binding_agree():
