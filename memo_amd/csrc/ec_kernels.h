@@ -22,9 +22,6 @@
 #ifndef MEMO_EC_DECODE_LDS
 #define MEMO_EC_DECODE_LDS 0
 #endif
-#ifndef MEMO_EC_MAC_WOUTER
-#define MEMO_EC_MAC_WOUTER 0
-#endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif

@@ -161,45 +161,6 @@ __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl
 template <int KC, int R>
 __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
                                           const uint32_t* tab, uint32_t kpad, uint32_t j0) {
-#if MEMO_EC_MAC_WOUTER
-  // dword-outer order: 6 selector registers live instead of 24; the
-  // broadcast tables are re-read from LDS per dword (an opaque offset keeps
-  // the compiler from caching all R pairs of tables in registers).
-#pragma unroll
-  for (int g = 0; g < KC; g += 2) {
-    const bool two = g + 1 < KC;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const uint32_t xa = w == 0 ? d[g].x : w == 1 ? d[g].y : w == 2 ? d[g].z : d[g].w;
-      const Sel sa = make_sel(xa);
-      Sel sb{};
-      if (two) {
-        const uint32_t xb = w == 0 ? d[g + 1].x : w == 1 ? d[g + 1].y : w == 2 ? d[g + 1].z : d[g + 1].w;
-        sb = make_sel(xb);
-      }
-      uint32_t off = (j0 + g) * 8;
-      asm volatile("" : "+v"(off));
-#pragma unroll
-      for (int i = 0; i < R; ++i) {
-        const uint32_t* tp = tab + off + i * kpad * 8;
-        const Tab ta = read_tab(tp);
-        uint32_t al, am, ah;
-        lookups(sa, ta, al, am, ah);
-        if (two) {
-          const Tab tb = read_tab(tp + 8);
-          uint32_t bl, bm, bh;
-          lookups(sb, tb, bl, bm, bh);
-          const uint32_t x = xor3(acc[i][w], al, am);
-          const uint32_t y = xor3(ah, bl, bm);
-          acc[i][w] = xor3(x, y, bh);
-        } else {
-          acc[i][w] = xor3(acc[i][w], al, am) ^ ah;
-        }
-      }
-    }
-  }
-  return;
-#endif
 #pragma unroll
   for (int g = 0; g < KC; g += MAC_PAIR ? 2 : 1) {
     const bool two = MAC_PAIR && g + 1 < KC;
