@@ -46,6 +46,9 @@ def lib():
         L.memo_oracle_decode_matrix.argtypes = [ctypes.c_int, ctypes.c_int, u8p, u8p, ctypes.c_int, u8p]
         L.memo_oracle_encode.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p]
         L.memo_oracle_encode_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, ctypes.c_int]
+        L.memo_oracle_encode_simd_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p,
+                                                 ctypes.c_int, ctypes.c_int]
+        L.memo_oracle_simd_isa.argtypes = []
         L.memo_oracle_rebuild.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, u8p, ctypes.c_int, u8p]
         L.memo_oracle_rebuild_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, u8p,
                                              ctypes.c_int, u8p, ctypes.c_int]
@@ -121,6 +124,35 @@ def encode(k, m, S, data, threads=1):
     if rc:
         raise ValueError("encode rc=%d" % rc)
     return par
+
+
+def aligned_empty(shape, align=64):
+    """uint8 array whose data pointer is `align`-byte aligned (numpy only
+    guarantees 16): lets encode_simd use streaming stores."""
+    nb = int(np.prod(shape))
+    raw = np.empty(nb + align, dtype=np.uint8)
+    off = (-raw.ctypes.data) % align
+    return raw[off:off + nb].reshape(shape)
+
+
+SIMD_ISA = {0: "scalar", 1: "avx2-pshufb", 2: "gfni-avx512"}
+
+
+def simd_isa():
+    """Best vector ISA of this host for encode_simd (0 scalar, 1 AVX2, 2 GFNI)."""
+    return lib().memo_oracle_simd_isa()
+
+
+def encode_simd(k, m, S, data, threads=1, isa=-1, out=None):
+    """Vectorised encode (rs_simd.c), same bytes as encode(); returns
+    (parity, isa_used)."""
+    data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1, k * S)
+    n = data.shape[0]
+    par = np.zeros((n, m * S), dtype=np.uint8) if out is None else out
+    used = lib().memo_oracle_encode_simd_mt(k, m, S, n, _p(data), _p(par), threads, isa)
+    if used < 0:
+        raise ValueError("encode_simd rejected k=%d m=%d" % (k, m))
+    return par, used
 
 
 def rebuild(k, m, S, surv_idx, surv, lost_idx, threads=1):

@@ -90,6 +90,30 @@ def test_encode_rebuild_vs_oracle(codec, O, k, m):
             assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
 
 
+def test_c1_full_size_vs_oracle(codec, O):
+    """BASELINE.json C1 at its full size: RS(3,2) encode + rebuild of 1000 x
+    64 KiB blocks, e in {1, 2} random erasures per block, bit-exact against
+    the oracle (the whole batch, not a sample)."""
+    k, m, B, n = 3, 2, 65536, 1000
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    want = O.encode(k, m, S, data, threads=4)
+    d = fill(codec, 0, n, B, k, S)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    codec.synchronize()
+    assert np.array_equal(host(d), data)
+    assert np.array_equal(host(p), want)
+    for e in (1, 2):
+        s, l = O.erasures(SEED, 0, n, k, m, e)
+        surv = empty(n, k * S)
+        codec.gather_shards(k, m, S, n, d, p, dev(s), surv)
+        out = empty(n, e * S)
+        codec.rebuild(k, m, dev(s), surv, dev(l), out)
+        codec.synchronize()
+        assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), e
+
+
 @pytest.mark.parametrize("k,m", [(3, 2), (4, 2)])
 def test_every_erasure_pattern_in_one_batch(codec, O, k, m):
     """Each block of the batch has a different erasure pattern (per-block

@@ -124,3 +124,39 @@ def test_threaded_baseline_matches_scalar(O):
 def test_singular_survivors_rejected(O):
     with pytest.raises(ValueError):
         O.decode_matrix(4, 2, [0, 1, 1, 2], [3])
+
+
+@pytest.mark.parametrize("k,m,S,n", [(10, 4, 104896, 3), (3, 2, 21888, 5), (16, 4, 256, 33),
+                                     (4, 2, 1000, 7), (1, 1, 64, 3), (64, 16, 192, 2),
+                                     (5, 3, 33, 4)])
+def test_vectorised_baseline_matches_scalar(O, k, m, S, n):
+    """oracle/rs_simd.c (the CPU baseline bench.py times) is bit-exact with
+    the scalar oracle on every ISA this host has, aligned (streaming stores)
+    and unaligned outputs, and odd shard sizes (scalar tail)."""
+    rng = np.random.default_rng(k * 100 + m)
+    data = O.aligned_empty((n, k * S))
+    data[:] = rng.integers(0, 256, (n, k * S), dtype=np.uint8)
+    ref = O.encode(k, m, S, data)
+    for isa in range(O.simd_isa() + 1):
+        out = O.aligned_empty((n, m * S))
+        par, used = O.encode_simd(k, m, S, data, threads=3, isa=isa, out=out)
+        assert used == isa and np.array_equal(par, ref), (isa, k, m, S)
+        par, _ = O.encode_simd(k, m, S, data, threads=2, isa=isa)
+        assert np.array_equal(par, ref), (isa, "unaligned")
+
+
+def test_c1_round_trip(O):
+    """BASELINE.json C1, the reference-runnable CPU case: RS(3,2) encode +
+    rebuild of 1000 x 64 KiB blocks with e in {1, 2} random erasures per
+    block; the rebuilt shards are bit-exact."""
+    k, m, B, n = 3, 2, 65536, 1000
+    S = O.shard_size(B, k)
+    assert S == 21888
+    data = O.fill_blocks(0x6D656D6F, 0, n, B, k, S)
+    par = O.encode(k, m, S, data, threads=4)
+    for e in (1, 2):
+        surv, lost = O.erasures(0x6D656D6F, 0, n, k, m, e)
+        shards = np.concatenate([data.reshape(n, k, S), par.reshape(n, m, S)], axis=1)
+        got = O.rebuild(k, m, S, surv, O.gather(k, m, S, data, par, surv), lost, threads=4)
+        want = np.take_along_axis(shards, lost.astype(np.int64)[:, :, None], axis=1)
+        assert np.array_equal(got.reshape(n, e, S), want)
