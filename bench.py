@@ -255,6 +255,15 @@ def main():
         except Exception:
             pass
 
+    # Measured HBM reference on this box: a device-to-device
+    # copy of the same data bytes on the same stream (read + write).
+    scratch = torch.empty_like(data)
+    _, cms = timed_launches(torch, lambda: scratch.copy_(data), 5, 2, None, stream)
+    copy_gbs = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
+    result["roofline"]["copy_GBs"] = round(copy_gbs, 1)
+    result["roofline"]["frac_of_copy"] = round(achieved / copy_gbs, 4)
+    del scratch
+
     if not args.no_rebuild and e > 0:
         s_idx, l_idx = ec.erasures(SEED, first_block, n, k, m, e)
         sd = torch.from_numpy(s_idx).cuda()

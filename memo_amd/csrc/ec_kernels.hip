@@ -730,30 +730,45 @@ __global__ void __launch_bounds__(256) sha256_kernel(Sha256Args a) {
   const uint64_t c_lo = (P + 63) / 64;
   const uint64_t c_hi = (P + L) / 64;
   const uint64_t nchunks = padded / 64;
-  for (uint64_t c = 0; c < nchunks; ++c) {
+  const uint64_t f_lo = fast ? c_lo : nchunks, f_hi = fast && c_hi > c_lo ? c_hi : f_lo;
+  auto slow_chunk = [&](uint64_t c) {
     uint32_t w[16];
-    if (fast && c >= c_lo && c < c_hi) {
-      const uint4* q = reinterpret_cast<const uint4*>(body + (c * 64 - P));
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(q + v));
-        w[4 * v + 0] = __builtin_bswap32(x.x);
-        w[4 * v + 1] = __builtin_bswap32(x.y);
-        w[4 * v + 2] = __builtin_bswap32(x.z);
-        w[4 * v + 3] = __builtin_bswap32(x.w);
-      }
-    } else {
-#pragma unroll
-      for (int t = 0; t < 16; ++t) {
-        const uint64_t o = c * 64 + 4 * t;
-        w[t] = (sha_byte(pre, P, body, L, bits, padded, o) << 24) |
-               (sha_byte(pre, P, body, L, bits, padded, o + 1) << 16) |
-               (sha_byte(pre, P, body, L, bits, padded, o + 2) << 8) |
-               sha_byte(pre, P, body, L, bits, padded, o + 3);
-      }
+    for (int t = 0; t < 16; ++t) {
+      const uint64_t o = c * 64 + 4 * t;
+      w[t] = (sha_byte(pre, P, body, L, bits, padded, o) << 24) |
+             (sha_byte(pre, P, body, L, bits, padded, o + 1) << 16) |
+             (sha_byte(pre, P, body, L, bits, padded, o + 2) << 8) |
+             sha_byte(pre, P, body, L, bits, padded, o + 3);
     }
     sha256_compress(h, w);
+  };
+  for (uint64_t c = 0; c < f_lo && c < nchunks; ++c) slow_chunk(c);
+  if (f_lo < f_hi) {
+    // Interior chunks: the next chunk's four dwordx4 loads are issued before
+    // this chunk's 64 rounds, so their latency hides behind the round chain.
+    const u32x4* q = reinterpret_cast<const u32x4*>(body + (f_lo * 64 - P));
+    u32x4 x[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) x[v] = __builtin_nontemporal_load(q + v);
+    for (uint64_t c = f_lo; c < f_hi; ++c) {
+      uint32_t w[16];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        w[4 * v + 0] = __builtin_bswap32(x[v].x);
+        w[4 * v + 1] = __builtin_bswap32(x[v].y);
+        w[4 * v + 2] = __builtin_bswap32(x[v].z);
+        w[4 * v + 3] = __builtin_bswap32(x[v].w);
+      }
+      q += 4;
+      if (c + 1 < f_hi) {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) x[v] = __builtin_nontemporal_load(q + v);
+      }
+      sha256_compress(h, w);
+    }
   }
+  for (uint64_t c = f_hi; c < nchunks; ++c) slow_chunk(c);
   uint32_t* out = reinterpret_cast<uint32_t*>(a.digest + i * 32);
 #pragma unroll
   for (int t = 0; t < 8; ++t) out[t] = __builtin_bswap32(h[t]);
