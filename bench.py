@@ -35,8 +35,10 @@ METRIC = "GiB/s RS(k,m) encode+rebuild, device-resident batched blocks; % HBM ro
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # ~60 ms of back-to-back launches: the MI355X's clocks dip a few launches
+    # into a burst and take ~40 launches to settle (profiles/r01_clock_ramp.jsonl)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=60)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
@@ -89,7 +91,7 @@ def max_over_ranks(torch, dist, x):
     return float(t.item())
 
 
-def sweep(torch, ec, codec, stream, gib, steps):
+def sweep(torch, ec, codec, stream, gib, steps, warmup):
     """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
     ~gib GiB of payload per point, one encode launch per step; then the same
     12 smaller groups fused into one launch (memo_ec_encode_segments)."""
@@ -101,7 +103,7 @@ def sweep(torch, ec, codec, stream, gib, steps):
             d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
             p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
             codec.fill_blocks(SEED, 0, n, B, k, S, d)
-            _, kms = timed_launches(torch, lambda: codec.encode(k, m, d, p), steps, 2, None, stream)
+            _, kms = timed_launches(torch, lambda: codec.encode(k, m, d, p), steps, warmup, None, stream)
             ms = float(np.mean(kms))
             alg = (k + m) * S * n
             points.append({"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
@@ -119,7 +121,7 @@ def sweep(torch, ec, codec, stream, gib, steps):
             segs.append((k, m, S, n, d, p))
             alg += (k + m) * S * n
             pay += n * B
-    _, kms = timed_launches(torch, lambda: codec.encode_segments(segs), steps, 2, None, stream)
+    _, kms = timed_launches(torch, lambda: codec.encode_segments(segs), steps, warmup, None, stream)
     ms = float(np.mean(kms))
     fused = {"segments": len(segs), "kernel_ms": round(ms, 4),
              "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
@@ -241,6 +243,8 @@ def main():
                      "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
                      "traffic": None, "bytes_per_launch": alg_bytes,
                      "kernel_ms_avg": round(kavg_ms, 4), "kernel_ms_min": round(min(kms), 4),
+                     "kernel_ms_median": round(float(np.median(kms)), 4),
+                     "kernel_ms_first_last": [round(kms[0], 4), round(kms[-1], 4)],
                      "kernel_ms_max_over_ranks": round(kavg_ms_max, 4),
                      "read_only_frac": round(k * S * n / (kavg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
     }
@@ -258,7 +262,7 @@ def main():
     # Measured HBM reference on this box: a device-to-device
     # copy of the same data bytes on the same stream (read + write).
     scratch = torch.empty_like(data)
-    _, cms = timed_launches(torch, lambda: scratch.copy_(data), 5, 2, None, stream)
+    _, cms = timed_launches(torch, lambda: scratch.copy_(data), 10, 30, None, stream)
     copy_gbs = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
     result["roofline"]["copy_GBs"] = round(copy_gbs, 1)
     result["roofline"]["frac_of_copy"] = round(achieved / copy_gbs, 4)
@@ -274,7 +278,7 @@ def main():
         want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
         codec.gather_shards(k, m, S, n, data, par, ld, want)
         reb = lambda: codec.rebuild(k, m, sd, surv, ld, out)  # noqa: E731
-        rwall, rkms = timed_launches(torch, reb, max(1, args.steps // 2), 2, dist, stream)
+        rwall, rkms = timed_launches(torch, reb, max(1, args.steps // 2), args.warmup, dist, stream)
         codec.synchronize()
         ok = bool(torch.equal(out, want))
         rwall = max_over_ranks(torch, dist, rwall)
@@ -353,7 +357,7 @@ def main():
 
     if args.sweep and world == 1:
         del data, par
-        result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4))
+        result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4), args.warmup)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

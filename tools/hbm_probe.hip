@@ -83,23 +83,28 @@ __global__ void __launch_bounds__(256) k_shards(const uint8_t* in, uint8_t* out,
   }
 }
 
+// Median launch time over `iters` back-to-back launches after 60 untimed
+// back-to-back warmup launches: the clocks dip a few launches into a burst
+// and settle after ~40 (profiles/r01_clock_ramp.jsonl), so neither a single
+// warmup launch nor a sync between launches measures the steady state.
 template <typename F>
 static float time_ms(F f, int iters) {
-  hipEvent_t a, b;
-  CHK(hipEventCreate(&a));
-  CHK(hipEventCreate(&b));
-  f();
+  std::vector<hipEvent_t> ev(2 * iters);
+  for (auto& evt : ev) CHK(hipEventCreate(&evt));
+  for (int i = 0; i < 60; ++i) f();
+  for (int i = 0; i < iters; ++i) {
+    CHK(hipEventRecord(ev[2 * i]));
+    f();
+    CHK(hipEventRecord(ev[2 * i + 1]));
+  }
   CHK(hipDeviceSynchronize());
   std::vector<float> ts;
   for (int i = 0; i < iters; ++i) {
-    CHK(hipEventRecord(a));
-    f();
-    CHK(hipEventRecord(b));
-    CHK(hipEventSynchronize(b));
     float ms;
-    CHK(hipEventElapsedTime(&ms, a, b));
+    CHK(hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]));
     ts.push_back(ms);
   }
+  for (auto& evt : ev) CHK(hipEventDestroy(evt));
   std::sort(ts.begin(), ts.end());
   return ts[ts.size() / 2];
 }
@@ -160,7 +165,7 @@ int main() {
   CHK(hipMemset(in, 1, bytes));
   CHK(hipMemset(out, 0, bytes));
   const size_t n4 = bytes / 16;
-  const int iters = 10;
+  const int iters = 20;
   for (int grid : {65536}) {
     float t;
     t = time_ms([&] { k_copy<false><<<grid, 256>>>((u32x4*)in, (u32x4*)out, n4); }, iters);

@@ -6,7 +6,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${ARGS:---steps 10 --warmup 2 --no-cpu --no-e2e}
+ARGS=${ARGS:---no-cpu --no-e2e}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T -d $OUT/trace -o trace -f csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T -d $OUT/fetch -o fetch -f csv -- python3 bench.py $ARGS --no-rebuild > $OUT/fetch.log 2>&1 || exit $?

@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--sets", type=int, default=4)
     ap.add_argument("--seconds", type=float, default=40.0)
     ap.add_argument("--launches", type=int, default=5)
+    ap.add_argument("--ramp", action="store_true",
+                    help="per-launch times of back-to-back encodes after an idle gap")
     ap.add_argument("--phases", action="store_true",
                     help="diagonal timings between phases of other traffic (read, copy, cross pairs)")
     ap.add_argument("--cross", action="store_true",
@@ -64,6 +66,23 @@ def main():
             for i, (d, p) in enumerate(sets):
                 row["set%d" % i] = round(alg / (timed(lambda: c.encode(k, m, d, p)) * 1e-3) / 8e12, 4)
             print(json.dumps(row), flush=True)
+
+    if a.ramp:
+        d, p = sets[0]
+        for idle in (2.0, 0.5, 0.1, 0.02):
+            time.sleep(idle)
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(120)]
+            for x, y in ev:
+                x.record(st)
+                c.encode(k, m, d, p)
+                y.record(st)
+            torch.cuda.synchronize()
+            fr = [round(alg / (x.elapsed_time(y) * 1e-3) / 8e12, 3) for x, y in ev]
+            print(json.dumps({"idle_s": idle, "first_20": fr[:20],
+                              "mean_by_10": [round(float(np.mean(fr[i:i + 10])), 4)
+                                             for i in range(0, 120, 10)]}), flush=True)
+        return
 
     if a.phases:
         diag("A-initial")
