@@ -406,45 +406,50 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
 
 // Shards of block `a` from the nodes in lookup order, in waves, until `want`
 // distinct valid shards are in hand.  Invalid shards count as erasures.
+// parallel = false fetches node by node (for callers already on the pool).
 std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
                                                                     bool& any_down,
-                                                                    ShardHeader* hdr) {
+                                                                    ShardHeader* hdr,
+                                                                    bool parallel) {
   const int total = o_.k + o_.m;
   auto nodes = overlay_.lookup(a, (int)overlay_.nodes().size());
   std::map<int, Buffer> got;
   std::mutex gm;
   any_down = false;
   size_t next = 0;
+  auto from_node = [&](const std::shared_ptr<Node>& nd) {
+    for (int i = 0; i < total; ++i) {
+      {
+        std::lock_guard<std::mutex> g(gm);
+        if (got.count(i)) continue;
+      }
+      Buffer wire;
+      try {
+        wire = nd->fetch(shard_key(a, i));
+      } catch (Unavailable&) {
+        std::lock_guard<std::mutex> g(gm);
+        any_down = true;
+        return;
+      } catch (silo::MissingKey&) {
+        continue;
+      }
+      try {
+        ShardHeader h = decode_shard(wire, nullptr);
+        if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) continue;
+        std::lock_guard<std::mutex> g(gm);
+        if (hdr && got.empty()) *hdr = h;
+        got.emplace(i, std::move(wire));
+      } catch (ValidationFailed&) {
+        // corrupted shard: an erasure
+      }
+    }
+  };
   while ((int)got.size() < want && next < nodes.size()) {
     const size_t wave = std::min(nodes.size() - next, (size_t)std::max(total, 1));
-    pool_.parallel_for(wave, [&](size_t w) {
-      auto& nd = nodes[next + w];
-      for (int i = 0; i < total; ++i) {
-        {
-          std::lock_guard<std::mutex> g(gm);
-          if (got.count(i)) continue;
-        }
-        Buffer wire;
-        try {
-          wire = nd->fetch(shard_key(a, i));
-        } catch (Unavailable&) {
-          std::lock_guard<std::mutex> g(gm);
-          any_down = true;
-          return;
-        } catch (silo::MissingKey&) {
-          continue;
-        }
-        try {
-          ShardHeader h = decode_shard(wire, nullptr);
-          if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) continue;
-          std::lock_guard<std::mutex> g(gm);
-          if (hdr && got.empty()) *hdr = h;
-          got.emplace(i, std::move(wire));
-        } catch (ValidationFailed&) {
-          // corrupted shard: an erasure
-        }
-      }
-    });
+    if (parallel)
+      pool_.parallel_for(wave, [&](size_t w) { from_node(nodes[next + w]); });
+    else
+      for (size_t w = 0; w < wave && (int)got.size() < want; ++w) from_node(nodes[next + w]);
     next += wave;
   }
   std::vector<std::pair<int, Buffer>> out;
@@ -452,57 +457,142 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   return out;
 }
 
-std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
-  if (a.mutable_block()) return backend_->fetch(a);
+ErasureConsensus::Gathered ErasureConsensus::collect(const Address& a, bool parallel) {
+  Gathered g;
   const int k = o_.k;
-  bool any_down = false;
-  ShardHeader h;
-  auto shards = gather_shards(a, k, any_down, &h);
-  if (shards.empty()) {
-    if (any_down) throw TooFewPeers("erasure: no shard reachable for " + a.hex());
-    throw MissingBlock("missing block " + a.hex());
-  }
-  if ((int)shards.size() < k)
-    throw TooFewPeers("erasure: " + std::to_string(shards.size()) + " shards reachable, need " +
-                      std::to_string(k));
-  const size_t S = h.shard_size;
-  std::sort(shards.begin(), shards.end(),
-            [](const auto& x, const auto& y) { return x.first < y.first; });
-  shards.resize(k);  // data shards first (sorted), then parity
-  Buffer block((size_t)k * S);
-  std::vector<int> have(k, -1);
-  for (size_t s = 0; s < shards.size(); ++s)
-    if (shards[s].first < k) have[shards[s].first] = (int)s;
-  std::vector<uint8_t> lost;
-  for (int j = 0; j < k; ++j) {
-    if (have[j] >= 0)
-      std::memcpy(block.data() + (size_t)j * S, shards[have[j]].second.data() + ShardHeader::kSize, S);
-    else
-      lost.push_back((uint8_t)j);
-  }
-  if (!lost.empty()) {
-    // systematic shards missing: rebuild them from the k survivors (GPU)
-    std::vector<uint8_t> sidx(k);
-    Buffer surv((size_t)k * S);
-    for (int s = 0; s < k; ++s) {
-      sidx[s] = (uint8_t)shards[s].first;
-      std::memcpy(surv.data() + (size_t)s * S, shards[s].second.data() + ShardHeader::kSize, S);
+  try {
+    bool any_down = false;
+    g.shards = gather_shards(a, k, any_down, &g.h, parallel);
+    if (g.shards.empty()) {
+      if (any_down) throw TooFewPeers("erasure: no shard reachable for " + a.hex());
+      throw MissingBlock("missing block " + a.hex());
     }
-    Buffer out(lost.size() * S);
-    codec_.rebuild(k, o_.m, S, 1, sidx.data(), surv.data(), lost.data(), (int)lost.size(), out.data());
-    for (size_t r = 0; r < lost.size(); ++r)
-      std::memcpy(block.data() + (size_t)lost[r] * S, out.data() + r * S, S);
-    ++decoded_;
+    if ((int)g.shards.size() < k)
+      throw TooFewPeers("erasure: " + std::to_string(g.shards.size()) +
+                        " shards reachable, need " + std::to_string(k));
+    std::sort(g.shards.begin(), g.shards.end(),
+              [](const auto& x, const auto& y) { return x.first < y.first; });
+    g.shards.resize(k);  // data shards first (sorted), then parity
+    std::vector<bool> have(k, false);
+    for (auto& s : g.shards)
+      if (s.first < k) have[s.first] = true;
+    for (int j = 0; j < k; ++j)
+      if (!have[j]) g.lost.push_back((uint8_t)j);
+  } catch (Error&) {
+    g.err = std::current_exception();
   }
-  block.resize(h.block_size);
-  if (!chb_valid(a, h.salt, block))
+  return g;
+}
+
+std::unique_ptr<Block> ErasureConsensus::assemble(const Address& a, Gathered& g,
+                                                  const uint8_t* rebuilt, size_t stride) {
+  const int k = o_.k;
+  const size_t S = g.h.shard_size;
+  Buffer block((size_t)k * S);
+  for (auto& s : g.shards)
+    if (s.first < k)
+      std::memcpy(block.data() + (size_t)s.first * S, s.second.data() + ShardHeader::kSize, S);
+  for (size_t r = 0; r < g.lost.size(); ++r)
+    std::memcpy(block.data() + (size_t)g.lost[r] * S, rebuilt + r * stride, S);
+  block.resize(g.h.block_size);
+  if (!chb_valid(a, g.h.salt, block))
     throw ValidationFailed("erasure: reassembled block does not match its address");
   auto b = std::make_unique<Block>();
   b->address = a;
   b->data = std::move(block);
-  b->salt = h.salt;
+  b->salt = g.h.salt;
   ++fetched_;
   return b;
+}
+
+std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
+  if (a.mutable_block()) return backend_->fetch(a);
+  const int k = o_.k;
+  Gathered g = collect(a, true);
+  if (g.err) std::rethrow_exception(g.err);
+  Buffer out;
+  if (!g.lost.empty()) {
+    // systematic shards missing: rebuild them from the k survivors (GPU)
+    const size_t S = g.h.shard_size;
+    std::vector<uint8_t> sidx(k);
+    Buffer surv((size_t)k * S);
+    for (int s = 0; s < k; ++s) {
+      sidx[s] = (uint8_t)g.shards[s].first;
+      std::memcpy(surv.data() + (size_t)s * S, g.shards[s].second.data() + ShardHeader::kSize, S);
+    }
+    out.resize(g.lost.size() * S);
+    codec_.rebuild(k, o_.m, S, 1, sidx.data(), surv.data(), g.lost.data(), (int)g.lost.size(),
+                   out.data());
+    ++decoded_;
+  }
+  return assemble(a, g, out.data(), g.h.shard_size);
+}
+
+// Multi-address fetch: shards of all blocks gathered on the pool, then ONE
+// GPU rebuild per (shard-size bucket, erasure count) group of the blocks
+// that miss data shards (zero-padded to the group's largest shard), then
+// reassembly + CHB check on the pool; `res` is called in request order.
+void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
+  const int k = o_.k, m = o_.m;
+  const size_t n = addresses.size();
+  std::vector<std::unique_ptr<Block>> blocks(n);
+  std::vector<std::exception_ptr> errs(n);
+  std::vector<size_t> imm;
+  for (size_t i = 0; i < n; ++i) {
+    if (!addresses[i].mutable_block()) {
+      imm.push_back(i);
+      continue;
+    }
+    try {
+      blocks[i] = backend_->fetch(addresses[i]);
+    } catch (Error&) {
+      errs[i] = std::current_exception();
+    }
+  }
+  std::vector<Gathered> g(n);
+  pool_.parallel_for(imm.size(), [&](size_t t) { g[imm[t]] = collect(addresses[imm[t]], false); });
+  std::map<std::pair<int, size_t>, std::vector<size_t>> groups;
+  std::vector<size_t> direct;
+  for (size_t i : imm) {
+    if (g[i].err)
+      errs[i] = g[i].err;
+    else if (g[i].lost.empty())
+      direct.push_back(i);
+    else
+      groups[{size_bucket(g[i].h.shard_size), g[i].lost.size()}].push_back(i);
+  }
+  auto finish = [&](size_t i, const uint8_t* rebuilt, size_t stride) {
+    try {
+      blocks[i] = assemble(addresses[i], g[i], rebuilt, stride);
+    } catch (Error&) {
+      errs[i] = std::current_exception();
+    }
+  };
+  pool_.parallel_for(direct.size(), [&](size_t t) { finish(direct[t], nullptr, 0); });
+  for (auto& grp : groups) {
+    const int e = (int)grp.first.second;
+    auto& ids = grp.second;
+    for (size_t b0 = 0; b0 < ids.size(); b0 += o_.batch_max) {
+      const size_t nb = std::min<size_t>(o_.batch_max, ids.size() - b0);
+      size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
+      for (size_t bi = 0; bi < nb; ++bi) S = std::max(S, (size_t)g[ids[b0 + bi]].h.shard_size);
+      std::vector<uint8_t> sidx(nb * k), lidx(nb * e);
+      Buffer surv(nb * k * S, 0), out(nb * e * S);
+      pool_.parallel_for(nb, [&](size_t bi) {
+        Gathered& x = g[ids[b0 + bi]];
+        for (int s = 0; s < k; ++s) {
+          sidx[bi * k + s] = (uint8_t)x.shards[s].first;
+          std::memcpy(surv.data() + (bi * k + s) * S, x.shards[s].second.data() + ShardHeader::kSize,
+                      x.h.shard_size);
+        }
+        std::copy(x.lost.begin(), x.lost.end(), lidx.begin() + bi * e);
+      });
+      codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data());
+      decoded_ += nb;
+      pool_.parallel_for(nb, [&](size_t bi) { finish(ids[b0 + bi], out.data() + bi * e * S, S); });
+    }
+  }
+  for (size_t i = 0; i < n; ++i) res(addresses[i], std::move(blocks[i]), errs[i]);
 }
 
 void ErasureConsensus::_remove(const Address& a) {

@@ -9,7 +9,10 @@
 //   fetch  : replaces Details::_fetch (Paxos.cc:486-519): any k valid shards;
 //            the k data shards are concatenated as they are (systematic code),
 //            otherwise the missing ones are rebuilt on the GPU; the CHB address
-//            is re-checked on the reassembled block (CHB.cc:79-99);
+//            is re-checked on the reassembled block (CHB.cc:79-99).  The
+//            multi-address fetch (Consensus::fetch(vector<AddressVersion>,
+//            ReceiveBlock), Consensus.cc:101-124) decodes every block that
+//            needs it in one GPU call per shard-size bucket;
 //   repair : replaces _disappeared_evict / _rebalance (Paxos.cc:1012-1246):
 //            every shard held by an evicted node is rebuilt in GPU-sized
 //            batches and re-placed on a new owner.
@@ -125,6 +128,7 @@ class ErasureConsensus : public StackedConsensus {
  protected:
   void _store(const Block& b, StoreMode mode) override;
   std::unique_ptr<Block> _fetch(const Address& a) override;
+  void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) override;
   void _remove(const Address& a) override;
 
  private:
@@ -137,11 +141,23 @@ class ErasureConsensus : public StackedConsensus {
     const Block* block;
     std::promise<Buffer> parity;  // m x S
   };
+  // A block's shards in hand for a fetch, and its missing data shards.
+  struct Gathered {
+    ShardHeader h;
+    std::vector<std::pair<int, Buffer>> shards;  // the k used, sorted by index
+    std::vector<uint8_t> lost;                   // data-shard indices to rebuild
+    std::exception_ptr err;
+  };
+  Gathered collect(const Address& a, bool parallel);
+  // The block from g's data shards and, for g.lost[r], the S bytes at
+  // rebuilt + r * stride; checks the CHB address.
+  std::unique_ptr<Block> assemble(const Address& a, Gathered& g, const uint8_t* rebuilt,
+                                  size_t stride);
   Buffer padded(const Block& b, size_t S) const;
   void place(const Block& b, const Buffer& parity);
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
-                                                    ShardHeader* hdr);
+                                                    ShardHeader* hdr, bool parallel = true);
 
   Overlay& overlay_;
   ErasureOptions o_;

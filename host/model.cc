@@ -200,6 +200,20 @@ std::vector<std::shared_ptr<Node>> Overlay::lookup(const Address& address, int n
   return out;
 }
 
+// ------------------------------------------------------------- consensus
+void Consensus::_fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
+  for (auto& a : addresses) {
+    std::unique_ptr<Block> b;
+    try {
+      b = fetch(a);
+    } catch (Error&) {
+      res(a, nullptr, std::current_exception());
+      continue;
+    }
+    res(a, std::move(b), nullptr);
+  }
+}
+
 // ----------------------------------------------------------- replication
 namespace {
 Key replica_key(const Address& a) { return a; }

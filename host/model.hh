@@ -8,6 +8,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <exception>
 #include <functional>
 #include <map>
 #include <memory>
@@ -199,11 +200,20 @@ class Overlay {
 // redundancy plugin base.  store/fetch/remove dispatch to the virtuals.
 enum StoreMode { STORE_INSERT, STORE_UPDATE };
 
+// Model::ReceiveBlock (src/memo/model/Model.hh:199): called once per
+// requested address with the block, or with null and the exception.
+using ReceiveBlock =
+    std::function<void(const Address&, std::unique_ptr<Block>, std::exception_ptr)>;
+
 class Consensus {
  public:
   virtual ~Consensus() = default;
   void store(const Block& b, StoreMode mode = STORE_INSERT) { _store(b, mode); }
   std::unique_ptr<Block> fetch(const Address& a) { return _fetch(a); }
+  // Consensus::fetch(vector<AddressVersion>, ReceiveBlock) (Consensus.cc:101-106).
+  void fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
+    _fetch(addresses, res);
+  }
   void remove(const Address& a) { _remove(a); }
   // Consensus::redundancy / stats (Consensus.cc:350-357): JSON text.
   virtual std::string redundancy() const = 0;
@@ -212,6 +222,9 @@ class Consensus {
  protected:
   virtual void _store(const Block& b, StoreMode mode) = 0;
   virtual std::unique_ptr<Block> _fetch(const Address& a) = 0;
+  // Default: one fetch per address, errors passed to `res`
+  // (Consensus::_fetch, Consensus.cc:108-124).
+  virtual void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res);
   virtual void _remove(const Address& a) = 0;
 };
 
@@ -237,6 +250,7 @@ class ReplicationConsensus : public Consensus {
 
  protected:
   void _store(const Block& b, StoreMode mode) override;
+  using Consensus::_fetch;
   std::unique_ptr<Block> _fetch(const Address& a) override;
   void _remove(const Address& a) override;
 

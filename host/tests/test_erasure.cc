@@ -265,6 +265,79 @@ TEST(availability, true) {
   }
 }
 
+// Consensus::fetch(vector<AddressVersion>, ReceiveBlock) (Consensus.cc:101-124,
+// used by Model::multifetch): every requested address gets exactly one
+// callback, in request order, with the block or its exception; blocks that
+// miss data shards are decoded in one GPU call per shard-size bucket instead
+// of one call per block.
+TEST(multi_fetch_batches_decodes, true) {
+  Net net(24, 10, 4);
+  std::vector<Block> blocks;
+  for (int i = 0; i < 60; ++i)
+    blocks.push_back(make_chb(random_bytes((i % 3 == 0 ? 4000 : i % 3 == 1 ? 60000 : 900000) + i, 100 + i)));
+  net.ec->store_many(blocks);
+  Block mut = make_mutable(Address::random(flags::mutable_block), bytes("meta"));
+  net.ec->store(mut);
+  // two nodes down: many blocks lose data shards
+  int down = 0;
+  for (auto& n : net.nodes)
+    if (down < 2 && !n->silo->list().empty()) {
+      n->up = false;
+      ++down;
+    }
+  std::vector<Address> req;
+  for (auto& b : blocks) req.push_back(b.address);
+  const Address missing = make_chb(bytes("never stored")).address;
+  req.insert(req.begin() + 7, missing);
+  req.push_back(mut.address);
+  const uint64_t calls0 = net.ec->codec().rebuild_calls();
+  std::vector<Address> seen;
+  int ok = 0, missing_seen = 0;
+  net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr e) {
+    seen.push_back(a);
+    if (a == missing) {
+      CHECK(!b && e);
+      try {
+        std::rethrow_exception(e);
+      } catch (MissingBlock&) {  // as the single fetch: MissingBlock, or
+        ++missing_seen;          // TooFewPeers while owners are down
+      } catch (TooFewPeers&) {
+        ++missing_seen;
+      } catch (...) {
+      }
+      return;
+    }
+    CHECK(b && !e);
+    if (!b) return;
+    if (a == mut.address) {
+      CHECK(b->data == bytes("meta"));
+      ++ok;
+      return;
+    }
+    for (auto& x : blocks)
+      if (x.address == a) {
+        CHECK(b->data == x.data);
+        if (b->data == x.data) ++ok;
+      }
+  });
+  CHECK(seen == req);
+  CHECK(ok == 61);
+  CHECK(missing_seen == 1);
+  const uint64_t batch_calls = net.ec->codec().rebuild_calls() - calls0;
+  // single fetches decode block by block; the batch used at most one call
+  // per (size bucket, erasure count) group: 3 buckets x e in {1, 2}
+  size_t need_decode = 0;
+  for (auto& b : blocks) {
+    const uint64_t c = net.ec->codec().rebuild_calls();
+    CHECK(net.ec->fetch(b.address)->data == b.data);
+    need_decode += net.ec->codec().rebuild_calls() - c;
+  }
+  std::fprintf(stderr, "  %zu of 60 blocks needed a decode; the batched fetch used %llu GPU calls\n",
+               need_decode, (unsigned long long)batch_calls);
+  CHECK(need_decode > 6);
+  CHECK(batch_calls >= 1 && batch_calls <= 6);
+}
+
 // Corrupted shards are erasures: flip bytes in m shards, fetch still exact.
 TEST(corrupted_shards_are_erasures, true) {
   Net net(14, 10, 4);

@@ -476,7 +476,7 @@ __global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
   }
 }
 
-// Register-resident variant for k <= K (K in {4, 8, 16, 32}): lane l holds
+// Register-resident variant for k <= K (K in {4, 8, 10, 12, 16, 32}): lane l holds
 // column l of the K x 2K matrix [A | I] in VGPRs (A padded to K x K with an
 // identity block, whose inverse is the identity, so rows/columns >= k never
 // mix with the real ones).  Pivot rows and row factors are broadcast with
@@ -836,6 +836,10 @@ hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(decode_rows_reg_kernel<4>, dim3(grid), dim3(256), lds_reg, st, a);
   } else if (a.k <= 8 && !MEMO_EC_DECODE_LDS) {
     hipLaunchKernelGGL(decode_rows_reg_kernel<8>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else if (a.k <= 10 && !MEMO_EC_DECODE_LDS) {  // RS(10,m): no padding steps
+    hipLaunchKernelGGL(decode_rows_reg_kernel<10>, dim3(grid), dim3(256), lds_reg, st, a);
+  } else if (a.k <= 12 && !MEMO_EC_DECODE_LDS) {
+    hipLaunchKernelGGL(decode_rows_reg_kernel<12>, dim3(grid), dim3(256), lds_reg, st, a);
   } else if (a.k <= 16 && !MEMO_EC_DECODE_LDS) {
     hipLaunchKernelGGL(decode_rows_reg_kernel<16>, dim3(grid), dim3(256), lds_reg, st, a);
   } else if (a.k <= 32 && !MEMO_EC_DECODE_LDS) {
