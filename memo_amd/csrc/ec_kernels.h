@@ -15,9 +15,6 @@
 #ifndef MEMO_EC_MAC_WAVES
 #define MEMO_EC_MAC_WAVES 1
 #endif
-#ifndef MEMO_EC_MAC_XCD
-#define MEMO_EC_MAC_XCD 1
-#endif
 // 1: always use the LDS Gauss-Jordan kernel (the register one serves k <= 32)
 #ifndef MEMO_EC_DECODE_LDS
 #define MEMO_EC_DECODE_LDS 0
@@ -56,7 +53,7 @@ struct MacSeg {
 
 struct MacLaunch {
   uint32_t nseg;
-  uint32_t pad_;
+  uint32_t xcd;  // 1: XCD-contiguous tile order inside each segment (see gf_mac_kernel)
   MacSeg seg[MEMO_EC_MAX_SEGMENTS];
 };
 

@@ -292,22 +292,25 @@ __global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const Ma
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
 
   // Segment of this workgroup (uniform), then its tile.
-#if MEMO_EC_MAC_XCD
-  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs, so
-  // give XCD x a contiguous range of tiles (bijective for any grid size):
-  // neighbouring tiles, which share the 128-byte lines at their edges when
-  // S is not a multiple of 128, then meet in the same L2.  Speed only.
-  const uint32_t W = gridDim.x, q = W / 8, rr = W % 8;
-  const uint32_t x = blockIdx.x % 8, i8 = blockIdx.x / 8;
-  const uint32_t wg = x * q + (x < rr ? x : rr) + i8;
-#else
   const uint32_t wg = blockIdx.x;
-#endif
   uint32_t sid = 0;
   for (uint32_t s = 1; s < L.nseg; ++s)
     if (wg >= L.seg[s].wg_begin) sid = s;
   const MacSeg& sg = L.seg[sid];
-  const uint64_t tile = wg - sg.wg_begin;
+  // Segments start on a multiple of 8 (launch_plans); workgroups past a
+  // segment's tiles are alignment padding.
+  const uint32_t lw = wg - sg.wg_begin;
+  if (lw >= sg.tiles) return;
+  uint64_t tile = lw;
+  if (L.xcd) {
+    // XCD-aware order: the hardware deals workgroups round-robin over the 8
+    // XCDs, so give XCD x a contiguous range of each segment's tiles
+    // (bijective for any size): neighbouring tiles, which share the 128-byte
+    // lines at their edges when S is not a multiple of 128, then meet in the
+    // same L2, and every XCD gets 1/8 of every segment.  Speed only.
+    const uint32_t st = (uint32_t)sg.tiles, sq = st / 8, sr = st % 8, sx = lw % 8;
+    tile = sx * sq + (sx < sr ? sx : sr) + lw / 8;
+  }
   const uint32_t kin = sg.kin, kpad = sg.kpad;
   const uint32_t set_dw = R * kpad * 8;
 

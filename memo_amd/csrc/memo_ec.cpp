@@ -130,6 +130,16 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
 
 // Launch 1..MEMO_EC_MAX_SEGMENTS planned segments as one kernel, one tile
 // per workgroup.  All share KC and R (the common compile-time bounds).
+// Smallest segment (in tiles) that gets the XCD-contiguous order;
+// MEMO_EC_XCD_MIN_TILES overrides (tuning).
+uint64_t xcd_min_tiles() {
+  static const uint64_t v = [] {
+    const char* p = std::getenv("MEMO_EC_XCD_MIN_TILES");
+    return p ? std::strtoull(p, nullptr, 10) : (uint64_t)65536;
+  }();
+  return v;
+}
+
 int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   if (plans.empty()) return MEMO_EC_OK;
   MacLaunch L{};
@@ -140,6 +150,7 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   for (auto& p : plans) {
     if (p.KC != KC || p.R != R) return MEMO_EC_EINVAL;
     if (p.seg.tiles == 0) continue;
+    wg = (wg + 7) / 8 * 8;  // segments start on an XCD-round boundary
     p.seg.wg_begin = (uint32_t)wg;
     wg += p.seg.tiles;
     lds = std::max(lds, p.lds);
@@ -147,6 +158,11 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   }
   if (wg == 0) return MEMO_EC_OK;
   if (wg > 0x7fffffffull) return MEMO_EC_ERANGE;
+  // The XCD-contiguous tile order pays on large grids (C2, 105k workgroups:
+  // +4%) and costs a few % on grids of a few 10k.
+  uint64_t min_tiles = ~0ull;
+  for (uint32_t i = 0; i < L.nseg; ++i) min_tiles = std::min<uint64_t>(min_tiles, L.seg[i].tiles);
+  L.xcd = min_tiles >= xcd_min_tiles() ? 1u : 0u;
   if (lds > 160 * 1024) return MEMO_EC_ERANGE;
   return hip_rc(launch_mac(KC, R, L, (uint32_t)wg, lds, st));
 }

@@ -18,7 +18,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libmemo_ec.so")
+# MEMO_EC_LIB points the binding at another build of the same ABI (the
+# tuning variants of tools/build_variants.sh); default: the in-tree library.
+LIB_PATH = os.environ.get("MEMO_EC_LIB") or os.path.join(_HERE, "_lib", "libmemo_ec.so")
 
 HOST, HOST_PINNED, DEVICE = 0, 1, 2
 MAX_K, MAX_M, MAX_SEGMENTS = 64, 16, 12

@@ -18,6 +18,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--lib", default=None)
     ap.add_argument("--gib", type=float, default=4.0)
+    ap.add_argument("--scan", action="store_true",
+                    help="also time RS(10,4) 1 MiB encode over grid sizes (XCD-order threshold)")
     a = ap.parse_args()
     import torch
     from memo_amd import ec
@@ -65,6 +67,18 @@ def main():
            "separate_ms": round(float(np.median(sep)), 4),
            "separate_frac": round(alg / (np.median(sep) * 1e-3) / 8e12, 4),
            "fused_10_4_only_frac": round(alg10 / (np.median(f10) * 1e-3) / 8e12, 4)}
+    if a.scan:
+        k, m, B = 10, 4, 1 << 20
+        S = ec.shard_size(B, k)
+        for n in (256, 512, 1024, 2048, 4096, 8192):
+            d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+            p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+            c.fill_blocks(0x6D656D6F, 0, n, B, k, S, d)
+            ms = float(np.median(timed(lambda: c.encode(k, m, d, p), warm=max(60, 60 * 4096 // n),
+                                       iters=20)))
+            out["scan_n%d_tiles%d" % (n, n * S // 16 // 256)] = round((k + m) * S * n / (ms * 1e-3) / 8e12, 4)
+            del d, p
+    out["xcd_min_tiles"] = os.environ.get("MEMO_EC_XCD_MIN_TILES", "default")
     print(json.dumps(out), flush=True)
 
 
