@@ -320,6 +320,29 @@ def main():
             "workload": "RS(%d,%d) encode, %d x %d-byte blocks from host memory, parity back to "
                         "host memory (HtoD + kernel + DtoH, 3-stage stream pipeline)" % (k, m, ne, B),
             "unit": "GiB/s", "pinned": e2e["pinned"], "pageable": e2e["pageable"]}
+        # One-block host calls, as the plugin issues them for a lone store or
+        # a degraded read (pageable elle::Buffer in, out): latency, not rate.
+        lat = {}
+        for bb in (4096, B):
+            Sb = ec.shard_size(bb, k)
+            d1 = np.frombuffer(np.random.default_rng(1).bytes(k * Sb), np.uint8).reshape(1, -1).copy()
+            p1 = np.zeros((1, m * Sb), np.uint8)
+            s1 = np.arange(1, k + 1, dtype=np.uint8).reshape(1, k)
+            l1 = np.zeros((1, 1), np.uint8)
+            o1 = np.zeros((1, Sb), np.uint8)
+            for name, fn in (("encode", lambda: codec.encode(k, m, d1, p1)),
+                             ("rebuild_e1", lambda: codec.rebuild(k, m, s1, d1, l1, o1))):
+                for _ in range(20):
+                    fn()
+                ts = []
+                for _ in range(200):
+                    t = time.perf_counter()
+                    fn()
+                    ts.append(time.perf_counter() - t)
+                lat["%s_%dB_us" % (name, bb)] = round(float(np.median(ts)) * 1e6, 1)
+        result["host_call_latency"] = dict(
+            lat, note="median of 200 one-block calls from pageable host memory (copy in, kernels, "
+                      "copy out, synchronous), RS(%d,%d)" % (k, m))
         codec.set_stream(stream)
 
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -2,8 +2,8 @@
 //
 // Host side of the drop-in boundary: validates arguments, plans the
 // multiply-accumulate launch (ec_kernels.hip), runs device-resident calls
-// asynchronously on the ctx stream and host-memory calls through a
-// double-buffered HtoD -> kernel -> DtoH pipeline.  No CPU fallback exists:
+// asynchronously on the ctx stream and host-memory calls through a 3-slot
+// HtoD -> kernel -> DtoH stream pipeline.  No CPU fallback exists:
 // every byte of parity/rebuild output is produced by the HIP kernels.
 #include <hip/hip_runtime.h>
 
@@ -192,10 +192,16 @@ int encode_tables(memo_ec_ctx* ctx, int k, int m, int R, int KC, const uint32_t*
   return MEMO_EC_OK;
 }
 
+int sync_pipeline(memo_ec_ctx* ctx);
+
+// Grows the per-block table scratch.  Earlier rebuilds of this ctx (on its
+// current stream or the host pipeline) may still read the old buffer, so
+// those streams drain first; other contexts on the device are not waited for.
 int ensure_tabs(memo_ec_ctx* ctx, size_t bytes) {
   if (bytes <= ctx->tabs_cap) return MEMO_EC_OK;
   if (ctx->d_tabs) {
-    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_pipeline(ctx)) return rc;
     HIPCHK(hipFree(ctx->d_tabs));
     ctx->d_tabs = nullptr;
   }
