@@ -6,6 +6,9 @@
 
 #include "../../include/memo_ec.h"
 
+// Compile-time knobs.  Each is a measured alternative (DESIGN.md section
+// 4.1; tools/build_variants.sh builds them, tools/tune_mac.py compares them);
+// the defaults are the winners.
 #ifndef MEMO_EC_MAC_NT
 #define MEMO_EC_MAC_NT 1
 #endif

@@ -30,6 +30,7 @@ struct memo_ec_ctx {
   hipStream_t sh = nullptr, sk = nullptr, sd = nullptr;
   hipEvent_t ev_h[3] = {}, ev_k[3] = {}, ev_d[3] = {};
   uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
+  uint32_t* h_status = nullptr;   // pinned copy of d_status for host-memory calls
   uint32_t* d_tabs = nullptr;     // per-block product-table images (rebuild)
   size_t tabs_cap = 0;            // bytes
   struct TabEntry {
@@ -263,9 +264,16 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
 }
 
 // Largest batch (blocks) one MAC launch takes: tiles must fit a 31-bit grid.
+// MEMO_EC_MAX_LAUNCH_TILES lowers the bound so tests can reach the split
+// path without a 2^31-tile batch.
 size_t max_blocks_per_launch(size_t S) {
+  uint64_t limit = 0x7fffffffull - MAC_TILE;
+  if (const char* p = std::getenv("MEMO_EC_MAX_LAUNCH_TILES")) {
+    const uint64_t v = std::strtoull(p, nullptr, 10);
+    if (v >= 1 && v < limit) limit = v;
+  }
   const uint64_t per = (S / 16 + MAC_TILE - 1) / MAC_TILE + 1;
-  return (size_t)std::max<uint64_t>(1, (0x7fffffffull - MAC_TILE) / per);
+  return (size_t)std::max<uint64_t>(1, limit / per);
 }
 
 // Device-resident encode on stream st.
@@ -418,6 +426,7 @@ int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
       (rc = hip_rc(hipStreamCreateWithFlags(&c->sk, hipStreamNonBlocking))) ||
       (rc = hip_rc(hipStreamCreateWithFlags(&c->sd, hipStreamNonBlocking))) ||
       (rc = hip_rc(hipMalloc(&c->d_status, 256))) ||
+      (rc = hip_rc(hipHostMalloc(&c->h_status, 64, hipHostMallocDefault))) ||
       (rc = hip_rc(hipMemset(c->d_status, 0, 256)))) {
     memo_ec_ctx_destroy(c);
     return rc;
@@ -453,6 +462,7 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
   if (c->d_tabs) (void)hipFree(c->d_tabs);
   for (auto& e : c->enc_tabs) (void)hipFree(e.dev);
   if (c->d_status) (void)hipFree(c->d_status);
+  if (c->h_status) (void)hipHostFree(c->h_status);
   for (int i = 0; i < kSlots; ++i)
     for (auto ev : {c->ev_h[i], c->ev_k[i], c->ev_d[i]})
       if (ev) (void)hipEventDestroy(ev);
@@ -579,14 +589,27 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       },
       [&](int s, size_t b0, size_t cnt) -> int {
         uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + o_out;
-        return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + o_out, cnt * out_b, hipMemcpyDeviceToHost,
-                                     c->sd));
+        HIPCHK(hipMemcpyAsync(dst, c->d_slot[s] + o_out, cnt * out_b, hipMemcpyDeviceToHost, c->sd));
+        // the deferred-error word rides behind the last batch's output, so
+        // reading it costs no extra round trip
+        if (b0 + cnt == n)
+          HIPCHK(hipMemcpyAsync(c->h_status, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                c->sd));
+        return MEMO_EC_OK;
       },
       [&](int s, size_t b0, size_t cnt) {
         if (!pinned) par_memcpy(out + b0 * out_b, c->h_slot[s] + o_out, cnt * out_b);
       });
   if (rc) return rc;
-  return take_deferred(c);
+  const uint32_t st = *c->h_status;
+  if (st) {
+    HIPCHK(hipMemsetAsync(c->d_status, 0, sizeof(uint32_t), c->sd));
+    HIPCHK(hipStreamSynchronize(c->sd));
+  }
+  int drc = c->deferred;
+  c->deferred = 0;
+  if (drc == MEMO_EC_OK && (st & 1u)) drc = MEMO_EC_ESINGULAR;
+  return drc;
 }
 
 int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* segs) {

@@ -90,6 +90,30 @@ def test_encode_rebuild_vs_oracle(codec, O, k, m):
             assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
 
 
+def test_batches_split_across_launches(codec, O, monkeypatch):
+    """A batch larger than one launch's grid is split into several MAC
+    launches (memo_ec.cpp max_blocks_per_launch); the bound is lowered so the
+    split happens at a testable size.  Encode and rebuild, device and host."""
+    k, m, B, n = 10, 4, 1 << 20, 64
+    S = O.shard_size(B, k)
+    monkeypatch.setenv("MEMO_EC_MAX_LAUNCH_TILES", "600")  # 22 blocks per launch
+    data = O.fill_blocks(SEED, 9, n, B, k, S)
+    want = O.encode(k, m, S, data, threads=4)
+    p = empty(n, m * S)
+    codec.encode(k, m, dev(data), p)
+    codec.synchronize()
+    assert np.array_equal(host(p), want)
+    hp = np.zeros_like(want)
+    codec.encode(k, m, data, hp)
+    assert np.array_equal(hp, want)
+    s, l = O.erasures(SEED, 9, n, k, m, 3)
+    surv = O.gather(k, m, S, data, want, s)
+    out = empty(n, 3 * S)
+    codec.rebuild(k, m, dev(s), dev(surv), dev(l), out)
+    codec.synchronize()
+    assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
+
+
 def test_c1_full_size_vs_oracle(codec, O):
     """BASELINE.json C1 at its full size: RS(3,2) encode + rebuild of 1000 x
     64 KiB blocks, e in {1, 2} random erasures per block, bit-exact against
@@ -196,6 +220,38 @@ def test_singular_survivors_reported(codec):
         codec.synchronize()
     assert ei.value.code == -4
     codec.synchronize()  # error is cleared
+
+
+def test_singular_survivors_reported_host_paths(codec, O, monkeypatch):
+    """Host-memory rebuilds report a bad survivor set from any pipeline batch
+    (the status word is read behind the last batch), the good blocks are
+    still rebuilt, and the error does not leak into the next call."""
+    import torch
+    from memo_amd import ec
+    k, m, B, n = 4, 2, 1 << 16, 40
+    S = O.shard_size(B, k)
+    monkeypatch.setenv("MEMO_EC_PIPE_MB", "1")  # several pipeline batches
+    c2 = ec.Codec(0)  # the pipeline size is read at ctx creation
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    s, l = O.erasures(SEED, 0, n, k, m, 1)
+    surv = O.gather(k, m, S, data, par, s)
+    want = O.gather(k, m, S, data, par, l)
+    bad = s.copy()
+    bad[3, 1] = bad[3, 0]  # a duplicate survivor in the first batch
+    for pinned in (False, True):
+        sv = torch.from_numpy(surv).pin_memory() if pinned else surv
+        out = torch.zeros((n, S), dtype=torch.uint8).pin_memory() if pinned else np.zeros((n, S), np.uint8)
+        with pytest.raises(ec.MemoECError) as ei:
+            c2.rebuild(k, m, bad, sv, l, out)
+        assert ei.value.code == -4
+        got = np.asarray(out)
+        good = np.ones(n, bool)
+        good[3] = False
+        assert np.array_equal(got[good], want.reshape(n, S)[good])
+        c2.rebuild(k, m, s, sv, l, out)  # clean call afterwards: no stale error
+        assert np.array_equal(np.asarray(out), want.reshape(n, S))
+    del c2
 
 
 def test_noops_and_argument_errors(codec):
