@@ -323,15 +323,20 @@ size_t tab_bytes(int k, int e, size_t n) {
 }
 
 // Host-memory pipeline over batches of nb blocks.  Batch i uses slot i % 3:
-//   in(slot, b0, cnt)       host staging + HtoD copies on sh
-//   run(slot, b0, cnt, sk)  kernels on sk, after the slot's HtoD (event)
-//   out(slot, b0, cnt)      DtoH copies on sd, after the kernels (event)
+//   in(slot, b0, cnt, st)   host staging + HtoD copies on st
+//   run(slot, b0, cnt, st)  kernels on st, after the slot's HtoD
+//   out(slot, b0, cnt, st)  DtoH copies on st, after the kernels
 //   done(slot, b0, cnt)     host side after the DtoH (pageable copy-out)
-// so the HtoD of batch i+1 runs under the DtoH of batch i (PCIe duplex).
+// With several batches the three stages run on the copy-in, compute and
+// copy-out streams chained by events, so the HtoD of batch i+1 runs under
+// the DtoH of batch i (PCIe duplex).  A single batch has nothing to overlap
+// and runs on one stream, without the cross-stream event hops (latency).
 template <class In, class Run, class Out, class Done>
 int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, Done done) {
   size_t off[kSlots] = {}, cnt[kSlots] = {};
   const size_t nbatch = (n + nb - 1) / nb;
+  const bool one = nbatch == 1;
+  hipStream_t s_in = one ? c->sk : c->sh, s_out = one ? c->sk : c->sd;
   auto finish = [&](int s) -> int {
     if (!cnt[s]) return MEMO_EC_OK;
     HIPCHK(hipEventSynchronize(c->ev_d[s]));
@@ -343,14 +348,18 @@ int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, D
     const int s = (int)(bi % kSlots);
     if (int rc = finish(s)) return rc;
     const size_t b0 = bi * nb, cn = std::min(nb, n - b0);
-    if (int rc = in(s, b0, cn)) return rc;
-    HIPCHK(hipEventRecord(c->ev_h[s], c->sh));
-    HIPCHK(hipStreamWaitEvent(c->sk, c->ev_h[s], 0));
+    if (int rc = in(s, b0, cn, s_in)) return rc;
+    if (!one) {
+      HIPCHK(hipEventRecord(c->ev_h[s], c->sh));
+      HIPCHK(hipStreamWaitEvent(c->sk, c->ev_h[s], 0));
+    }
     if (int rc = run(s, b0, cn, c->sk)) return rc;
-    HIPCHK(hipEventRecord(c->ev_k[s], c->sk));
-    HIPCHK(hipStreamWaitEvent(c->sd, c->ev_k[s], 0));
-    if (int rc = out(s, b0, cn)) return rc;
-    HIPCHK(hipEventRecord(c->ev_d[s], c->sd));
+    if (!one) {
+      HIPCHK(hipEventRecord(c->ev_k[s], c->sk));
+      HIPCHK(hipStreamWaitEvent(c->sd, c->ev_k[s], 0));
+    }
+    if (int rc = out(s, b0, cn, s_out)) return rc;
+    HIPCHK(hipEventRecord(c->ev_d[s], s_out));
     off[s] = b0;
     cnt[s] = cn;
   }
@@ -506,21 +515,21 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   // slot layout (device and pageable bounce): [data nb*in_b | parity nb*out_b]
   return run_pipeline(
       c, n, nb,
-      [&](int s, size_t b0, size_t cnt) -> int {
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         const uint8_t* src = data + b0 * in_b;
         if (!pinned) {
           par_memcpy(c->h_slot[s], src, cnt * in_b);
           src = c->h_slot[s];
         }
-        return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, c->sh));
+        return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, st));
       },
       [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
         return encode_device(c, k, m, S, cnt, c->d_slot[s], c->d_slot[s] + nb * in_b, st);
       },
-      [&](int s, size_t b0, size_t cnt) -> int {
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* dst = pinned ? parity + b0 * out_b : c->h_slot[s] + nb * in_b;
         return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + nb * in_b, cnt * out_b,
-                                     hipMemcpyDeviceToHost, c->sd));
+                                     hipMemcpyDeviceToHost, st));
       },
       [&](int s, size_t b0, size_t cnt) {
         if (!pinned) par_memcpy(parity + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
@@ -569,32 +578,32 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
   const int rc = run_pipeline(
       c, n, nb,
-      [&](int s, size_t b0, size_t cnt) -> int {
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* h = c->h_slot[s];
         uint8_t* d = c->d_slot[s];
         std::memcpy(h + o_sidx, surv_idx + b0 * k, cnt * k);  // indices: always bounced
         std::memcpy(h + o_lidx, lost_idx + b0 * e, cnt * e);
-        HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx, nb * idx_b, hipMemcpyHostToDevice, c->sh));
+        HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx, nb * idx_b, hipMemcpyHostToDevice, st));
         const uint8_t* src = surv + b0 * in_b;
         if (!pinned) {
           par_memcpy(h, src, cnt * in_b);
           src = h;
         }
-        return hip_rc(hipMemcpyAsync(d, src, cnt * in_b, hipMemcpyHostToDevice, c->sh));
+        return hip_rc(hipMemcpyAsync(d, src, cnt * in_b, hipMemcpyHostToDevice, st));
       },
       [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
         uint8_t* d = c->d_slot[s];
         return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out, nullptr,
                               c->d_tabs + (size_t)s * tabs / 4, st);
       },
-      [&](int s, size_t b0, size_t cnt) -> int {
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + o_out;
-        HIPCHK(hipMemcpyAsync(dst, c->d_slot[s] + o_out, cnt * out_b, hipMemcpyDeviceToHost, c->sd));
+        HIPCHK(hipMemcpyAsync(dst, c->d_slot[s] + o_out, cnt * out_b, hipMemcpyDeviceToHost, st));
         // the deferred-error word rides behind the last batch's output, so
         // reading it costs no extra round trip
         if (b0 + cnt == n)
           HIPCHK(hipMemcpyAsync(c->h_status, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                c->sd));
+                                st));
         return MEMO_EC_OK;
       },
       [&](int s, size_t b0, size_t cnt) {
