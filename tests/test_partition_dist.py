@@ -75,3 +75,26 @@ def test_two_rank_partition_gloo():
     S = O.shard_size(B, k)
     whole = O.encode(k, m, S, O.fill_blocks(SEED, 0, n, B, k, S)).reshape(-1)
     assert np.array_equal(np.concatenate(parts), whole)
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_one_gpu():
+    """bench.py's N>1 path end to end on the one GPU of a test box: two
+    ranks under torch.distributed.run (gloo for the barrier/max, both ranks
+    on cuda:0), each encoding its own block range; rank 0 prints one JSON
+    line with the whole-job value.  The 8-GPU RCCL run is the driver's."""
+    import json
+    import subprocess
+    import sys
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--steps", "3", "--warmup", "2",
+           "--blocks", "64", "--no-cpu", "--no-e2e"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 128
+    assert res["value"] > 0 and res["rebuild"]["round_trip_bit_exact"]
