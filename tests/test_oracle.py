@@ -160,3 +160,28 @@ def test_c1_round_trip(O):
         got = O.rebuild(k, m, S, surv, O.gather(k, m, S, data, par, surv), lost, threads=4)
         want = np.take_along_axis(shards, lost.astype(np.int64)[:, :, None], axis=1)
         assert np.array_equal(got.reshape(n, e, S), want)
+
+
+# Randomised agreement of the two restatements (C oracle vs the numpy one,
+# which shares no code with it): any geometry, any block size, any seed.
+from hypothesis import HealthCheck, given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(k=st.integers(1, 24), m=st.integers(1, 8), B=st.integers(0, 6000),
+       seed=st.integers(0, 2**63 - 1), block=st.integers(0, 2**40), data=st.data())
+def test_two_restatements_agree(O, k, m, B, seed, block, data):
+    from oracle import rs_numpy as N
+    S = O.shard_size(B, k)
+    assert S == N.shard_size(B, k)
+    d = O.fill_blocks(seed, block, 1, B, k, S)
+    assert np.array_equal(d[0], N.fill_block(seed, block, B, k, S))
+    par = O.encode(k, m, S, d)
+    assert np.array_equal(par, N.encode(k, m, S, d))
+    e = data.draw(st.integers(1, m))
+    s, l = O.erasures(seed, block, 1, k, m, e)
+    ns, nl = N.erasures(seed, block, k, m, e)
+    assert list(s[0]) == list(ns) and list(l[0]) == list(nl)
+    assert np.array_equal(O.decode_matrix(k, m, s[0], l[0]), N.decode_matrix(k, m, s[0], l[0]))
+    got = O.rebuild(k, m, S, s, O.gather(k, m, S, d, par, s), l)
+    assert np.array_equal(got, O.gather(k, m, S, d, par, l))
