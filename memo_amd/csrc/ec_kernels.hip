@@ -518,6 +518,7 @@ __global__ void __launch_bounds__(256) decode_rows_reg_kernel(DecodeArgs a) {
     }
   }
 
+#ifndef MEMO_EC_DECODE_DIAG_NOGJ  // diagnostic build: skip the elimination (wrong rows)
 #pragma unroll
   for (int c = 0; c < K; ++c) {
     if (bad) break;
@@ -553,6 +554,7 @@ __global__ void __launch_bounds__(256) decode_rows_reg_kernel(DecodeArgs a) {
       if (f) m[r] ^= nz ? (uint32_t)ex[lc + lg[f]] : 0u;
     }
   }
+#endif
 
   // Right half, lane K+j, now holds column j of A^-1: inv[t][j] = m[t].
   for (uint32_t r = 0; r < e; ++r) {
