@@ -126,8 +126,10 @@ int memo_ec_decode_rows(memo_ec_ctx *ctx, int k, int m, size_t n,
                         const uint8_t *surv_idx, const uint8_t *lost_idx,
                         int e, uint8_t *rows);
 
-/* Fused encode of up to MEMO_EC_MAX_SEGMENTS device-resident segments with
- * different (k, m, S) in one launch.  Asynchronous on the ctx stream. */
+/* Batched encode of up to MEMO_EC_MAX_SEGMENTS device-resident segments
+ * with different (k, m, S): segments of one shard-chunk class (same
+ * specialised k) share one launch, classes run back to back.  Asynchronous
+ * on the ctx stream. */
 int memo_ec_encode_segments(memo_ec_ctx *ctx, int nseg,
                             const memo_ec_segment *segs);
 

@@ -22,6 +22,17 @@
 #ifndef MEMO_EC_DECODE_LDS
 #define MEMO_EC_DECODE_LDS 0
 #endif
+// 1: shard loads / output stores through buffer resources with the cache
+// policies below (gfx950 cpol: sc0 = 1, nt = 2, sc1 = 16)
+#ifndef MEMO_EC_MAC_BUF
+#define MEMO_EC_MAC_BUF 0
+#endif
+#ifndef MEMO_EC_MAC_LDAUX
+#define MEMO_EC_MAC_LDAUX 2
+#endif
+#ifndef MEMO_EC_MAC_STAUX
+#define MEMO_EC_MAC_STAUX 2
+#endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif

@@ -121,6 +121,22 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
   else *q = w;
 }
 
+// Buffer-resource access (uniform base in SGPRs, 32-bit lane offset, shard
+// offset as the scalar soffset) with an explicit cache policy (gfx950 cpol
+// bits: sc0 = 1, nt = 2, sc1 = 16).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0xffffffff, 0x00020000);
+}
+__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, MEMO_EC_MAC_LDAUX);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
+                                      uint4 v) {
+  const u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, MEMO_EC_MAC_STAUX);
+}
+
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -210,6 +226,7 @@ struct Unit {
   bool valid;
   const uint8_t* pin;
   uint8_t* pout;
+  uint32_t voff_in, voff_out;  // byte offsets from the tile's first block (buffer path)
 };
 
 __device__ __forceinline__ Unit locate(const MacSeg& sg, uint64_t tile) {
@@ -250,6 +267,8 @@ __device__ __forceinline__ Unit locate(const MacSeg& sg, uint64_t tile) {
   const uint64_t b = u.b_first + bo;
   u.pin = sg.in + b * sg.in_bstride + (uint64_t)cc * 16;
   u.pout = sg.out + b * sg.out_bstride + (uint64_t)cc * 16;
+  u.voff_in = (uint32_t)(bo * sg.in_bstride + (uint64_t)cc * 16);
+  u.voff_out = (uint32_t)(bo * sg.out_bstride + (uint64_t)cc * 16);
   return u;
 }
 
@@ -287,21 +306,19 @@ __device__ __forceinline__ void store_tables(const MacSeg& sg, const Unit& u, ui
   for (uint32_t t = threadIdx.x + 256u * MAC_TAB_REGS; t < total; t += 256) s_tab[t] = src[t];
 }
 
-template <int KC, int R, bool NT>
-__global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const MacLaunch L) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
-
-  // Segment of this workgroup (uniform), then its tile.
+// Segment of workgroup blockIdx.x and its tile (XCD-aware order); false for
+// the alignment padding past a segment's tiles.
+__device__ __forceinline__ bool seg_tile(const MacLaunch& L, uint32_t& sid, uint64_t& tile) {
   const uint32_t wg = blockIdx.x;
-  uint32_t sid = 0;
+  sid = 0;
   for (uint32_t s = 1; s < L.nseg; ++s)
     if (wg >= L.seg[s].wg_begin) sid = s;
   const MacSeg& sg = L.seg[sid];
   // Segments start on a multiple of 8 (launch_plans); workgroups past a
   // segment's tiles are alignment padding.
   const uint32_t lw = wg - sg.wg_begin;
-  if (lw >= sg.tiles) return;
-  uint64_t tile = lw;
+  if (lw >= sg.tiles) return false;
+  tile = lw;
   if (L.xcd) {
     // XCD-aware order: the hardware deals workgroups round-robin over the 8
     // XCDs, so give XCD x a contiguous range of each segment's tiles
@@ -311,6 +328,13 @@ __global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const Ma
     const uint32_t st = (uint32_t)sg.tiles, sq = st / 8, sr = st % 8, sx = lw % 8;
     tile = sx * sq + (sx < sr ? sx : sr) + lw / 8;
   }
+  return true;
+}
+
+// One tile of segment sg: KC is the straight-line shard chunk (kin == KC is
+// the hot path; other kin loop over chunks of KC shards).
+template <int KC, int R, bool NT>
+__device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32_t* s_tab) {
   const uint32_t kin = sg.kin, kpad = sg.kpad;
   const uint32_t set_dw = R * kpad * 8;
 
@@ -330,8 +354,14 @@ __global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const Ma
     uint32_t tv[MAC_TAB_REGS];
     load_tables(sg, u, set_dw, tv);
     uint4 d[KC];
+#if MEMO_EC_MAC_BUF
+    const __amdgpu_buffer_rsrc_t rin = rsrc_of(sg.in + u.b_first * sg.in_bstride);
+#pragma unroll
+    for (int g = 0; g < KC; ++g) d[g] = bld16(rin, u.voff_in, (uint32_t)(g * sg.in_sstride));
+#else
 #pragma unroll
     for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
+#endif
     store_tables(sg, u, set_dw, tv, s_tab);
 #else
     uint4 d[KC];
@@ -354,12 +384,30 @@ __global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const Ma
   }
 
   if (u.valid) {
+#if MEMO_EC_MAC_BUF
+    const __amdgpu_buffer_rsrc_t rout = rsrc_of(sg.out + u.b_first * sg.out_bstride);
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+      if ((uint32_t)i < sg.r)
+        bst16(rout, u.voff_out, (uint32_t)(i * sg.out_sstride),
+              make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+#else
 #pragma unroll
     for (int i = 0; i < R; ++i)
       if ((uint32_t)i < sg.r)
         st16<NT>(u.pout + (uint64_t)i * sg.out_sstride,
                  make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
+#endif
   }
+}
+
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const MacLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
+  uint32_t sid;
+  uint64_t tile;
+  if (!seg_tile(L, sid, tile)) return;
+  mac_tile<KC, R, NT>(L.seg[sid], tile, s_tab);
 }
 
 // ------------------------------------------------------------- decode rows

@@ -133,6 +133,13 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
 // per workgroup.  All share KC and R (the common compile-time bounds).
 // Smallest segment (in tiles) that gets the XCD-contiguous order;
 // MEMO_EC_XCD_MIN_TILES overrides (tuning).
+// Largest table LDS of a launch's segments.
+size_t lds_of(const std::vector<Plan>& plans) {
+  size_t lds = 0;
+  for (const auto& p : plans) lds = std::max(lds, p.lds);
+  return lds;
+}
+
 uint64_t xcd_min_tiles() {
   static const uint64_t v = [] {
     const char* p = std::getenv("MEMO_EC_XCD_MIN_TILES");
@@ -623,9 +630,15 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
 
 int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* segs) {
   if (!c || nseg < 0 || nseg > MEMO_EC_MAX_SEGMENTS || (nseg && !segs)) return MEMO_EC_EINVAL;
-  // common bounds: the specialised chunk when every segment has the same k,
-  // else 4; R = the largest m's bound (smaller m's rows are zero tables)
-  int KC = -1, R = 1;
+  // Segments are grouped by shard-chunk class (mac_kchunk(k)): each class is
+  // one launch of its own straight-line body, with R = the class's largest
+  // m bound (smaller m's rows are zero tables); the launches go back to back
+  // on the ctx stream.  One launch across classes would force every segment
+  // onto the 4-shard chunk loop: 72% of 8 TB/s on the C5 mix against 77% for
+  // per-class launches.  Everything is validated
+  // before anything is enqueued.
+  std::vector<int> classes;  // KC of each class, in order of first appearance
+  std::vector<int> cls_R;
   for (int i = 0; i < nseg; ++i) {
     if (int rc = check_km(segs[i].k, segs[i].m)) return rc;
     if (segs[i].m == 0 || segs[i].n == 0) continue;
@@ -633,22 +646,33 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
       return MEMO_EC_EINVAL;
     if (segs[i].n > max_blocks_per_launch(segs[i].S)) return MEMO_EC_ERANGE;
     const int kc = mac_kchunk(segs[i].k);
-    KC = (KC < 0 || KC == kc) ? kc : 4;
-    R = std::max(R, mac_rbound(segs[i].m));
+    size_t ci = 0;
+    while (ci < classes.size() && classes[ci] != kc) ++ci;
+    if (ci == classes.size()) {
+      classes.push_back(kc);
+      cls_R.push_back(1);
+    }
+    cls_R[ci] = std::max(cls_R[ci], mac_rbound(segs[i].m));
   }
-  if (KC < 0) return MEMO_EC_OK;
+  if (classes.empty()) return MEMO_EC_OK;
   DeviceGuard g(c->device);
-  std::vector<Plan> plans;
-  for (int i = 0; i < nseg; ++i) {
-    const auto& s = segs[i];
-    if (s.m == 0 || s.n == 0) continue;
-    const uint32_t* tab = nullptr;
-    if (int rc = encode_tables(c, s.k, s.m, R, KC, &tab)) return rc;
-    plans.push_back(plan_segment((uint32_t)s.k, (uint32_t)s.m, s.S, s.n, s.data,
-                                 (uint64_t)s.k * s.S, s.S, s.parity, (uint64_t)s.m * s.S, s.S,
-                                 tab, 0, KC, R));
+  std::vector<std::vector<Plan>> launches(classes.size());
+  for (size_t ci = 0; ci < classes.size(); ++ci) {
+    const int KC = classes[ci], R = cls_R[ci];
+    for (int i = 0; i < nseg; ++i) {
+      const auto& s = segs[i];
+      if (s.m == 0 || s.n == 0 || mac_kchunk(s.k) != KC) continue;
+      const uint32_t* tab = nullptr;
+      if (int rc = encode_tables(c, s.k, s.m, R, KC, &tab)) return rc;
+      launches[ci].push_back(plan_segment((uint32_t)s.k, (uint32_t)s.m, s.S, s.n, s.data,
+                                          (uint64_t)s.k * s.S, s.S, s.parity,
+                                          (uint64_t)s.m * s.S, s.S, tab, 0, KC, R));
+    }
+    if (lds_of(launches[ci]) > 160 * 1024) return MEMO_EC_ERANGE;
   }
-  return launch_plans(plans, c->stream);
+  for (auto& plans : launches)
+    if (int rc = launch_plans(plans, c->stream)) return rc;
+  return MEMO_EC_OK;
 }
 
 int memo_ec_sha256_batch(memo_ec_ctx* c, size_t n, const uint8_t* prefix, size_t prefix_len,

@@ -189,6 +189,26 @@ def test_mixed_segments_one_launch(codec, O):
         assert np.array_equal(host(p), w), (k, m, S)
 
 
+@pytest.mark.parametrize("codes", [
+    [(3, 2, 5000, 9), (7, 3, 70000, 4), (20, 4, 300000, 3), (12, 1, 4096, 40), (16, 4, 4096, 33)],
+    [(4, 2, 4096, 5), (10, 6, 100000, 2), (2, 1, 64, 300)],  # R > 4: the chunk loop
+])
+def test_mixed_segments_any_k(codec, O, codes):
+    """Mixed k in one launch, including k outside {4, 10, 16}, k > 16 and
+    m > 4 (gf_mac_multi_kernel's variable-k body and its fallbacks)."""
+    segs, want = [], []
+    for i, (k, m, B, n) in enumerate(codes):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 1000 + 100 * i, n, B, k, S)
+        p = empty(n, m * S)
+        segs.append((k, m, S, n, dev(data), p))
+        want.append(O.encode(k, m, S, data))
+    codec.encode_segments(segs)
+    codec.synchronize()
+    for (k, m, S, n, d, p), w in zip(segs, want):
+        assert np.array_equal(host(p), w), (k, m, S)
+
+
 def test_host_memory_paths(codec, O):
     import torch
     k, m, B, n = 10, 4, 1 << 20, 70  # > one 64 MiB pipeline batch
