@@ -94,7 +94,9 @@ def max_over_ranks(torch, dist, x):
 def sweep(torch, ec, codec, stream, gib, steps, warmup):
     """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
     ~gib GiB of payload per point, one encode launch per step; then the same
-    12 smaller groups fused into one launch (memo_ec_encode_segments)."""
+    12 smaller groups as ONE memo_ec_encode_segments call (one launch per
+    shard-chunk class, back to back; timed from before the first launch to
+    after the last)."""
     points = []
     for (k, m) in [(4, 2), (10, 4), (16, 4)]:
         for B in [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20]:
@@ -127,7 +129,8 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup):
              "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
              "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
     return {"workload": "BASELINE.json C5: RS(k,m) encode per (k,m) x block size, ~%.1f GiB "
-                        "payload per point; fused = 12 mixed groups in one launch" % gib,
+                        "payload per point; fused = 12 mixed groups in one encode_segments call "
+                        "(one launch per code class)" % gib,
             "points": points, "fused": fused}
 
 
