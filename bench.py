@@ -134,6 +134,40 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup):
             "points": points, "fused": fused}
 
 
+def rebuild_small(torch, ec, codec, stream, steps, warmup):
+    """Small-block rebuild: 4 KiB blocks (~4 GiB of payload), 4 random
+    erasures per block, so every block has its own decode rows and a
+    256-column tile spans up to 17 blocks' tables.  Step = decode + MAC."""
+    res = {}
+    for (k, m) in [(10, 4), (16, 4)]:
+        B, n, e = 4096, 1 << 20, 4
+        S = ec.shard_size(B, k)
+        d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+        p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+        codec.fill_blocks(SEED, 0, n, B, k, S, d)
+        codec.encode(k, m, d, p)
+        s_idx, l_idx = ec.erasures(SEED, 0, n, k, m, e)
+        sd, ld = torch.from_numpy(s_idx).cuda(), torch.from_numpy(l_idx).cuda()
+        surv = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, d, p, ld, want)
+        del d, p
+        out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        _, kms = timed_launches(torch, lambda: codec.rebuild(k, m, sd, surv, ld, out),
+                                max(1, steps // 2), warmup, None, stream)
+        codec.synchronize()
+        ms = float(np.mean(kms))
+        alg = (k + e) * S * n
+        res["RS(%d,%d)" % (k, m)] = {
+            "blocks": n, "block_bytes": B, "shard_bytes": S, "erasures": e,
+            "step_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
+            "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "bit_exact": bool(torch.equal(out, want))}
+        del surv, out, want, sd, ld
+    return res
+
+
 def _rate(fn, nbytes, seconds):
     """GiB/s of repeated fn() passes over ~`seconds` (at least one pass)."""
     passes, t = 0, time.perf_counter()
@@ -296,9 +330,11 @@ def main():
             "step_ms_events": round(rk, 4),
             "achieved_GBs": round(rbytes / (rk * 1e-3) / 1e9, 1),
             "frac": round(rbytes / (rk * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-            "note": "step = decode-rows (batched GF inversion) + gf_mac_kernel",
+            "note": "step = decode_coef_kernel (closed-form decode rows) + gf_mac_kernel",
             "round_trip_bit_exact": ok}
         del surv, out, want
+        if world == 1:
+            result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps, args.warmup)
 
     if not args.no_e2e and world == 1:
         # PCIe-inclusive: blocks start and end in host memory (RPC socket in,

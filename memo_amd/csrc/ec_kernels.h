@@ -15,12 +15,8 @@
 #ifndef MEMO_EC_MAC_TABFIRST
 #define MEMO_EC_MAC_TABFIRST 1
 #endif
-#ifndef MEMO_EC_MAC_WAVES
-#define MEMO_EC_MAC_WAVES 1
-#endif
-// 1: always use the LDS Gauss-Jordan kernel (the register one serves k <= 32)
-#ifndef MEMO_EC_DECODE_LDS
-#define MEMO_EC_DECODE_LDS 0
+#ifndef MEMO_EC_MAC_W16
+#define MEMO_EC_MAC_W16 1
 #endif
 // 1: shard loads / output stores through buffer resources with the cache
 // policies below (gfx950 cpol: sc0 = 1, nt = 2, sc1 = 16)
@@ -36,6 +32,9 @@
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif
+#ifndef MEMO_EC_MAC_PAIR16
+#define MEMO_EC_MAC_PAIR16 1
+#endif
 
 namespace memo_ec {
 
@@ -45,6 +44,9 @@ constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
 constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
 // Table dwords per lane staged through registers ahead of the shard loads.
 constexpr int MAC_TAB_REGS = 2;
+// Coefficients per lane staged through registers (rebuild tables built in
+// LDS): 256 * 6 = 1536 = the flat-mapping LDS budget (48 KiB) / 32 B.
+constexpr int MAC_COEF_REGS = 6;
 // A tile = 256 16-byte columns = one workgroup of gf_mac_kernel.
 constexpr uint32_t MAC_TILE = 256;
 
@@ -56,6 +58,9 @@ struct MacSeg {
   uint64_t in_bstride, in_sstride;
   uint64_t out_bstride, out_sstride;
   uint64_t tab_bstride;   // dwords between blocks' images; 0 = one image for all
+  const uint8_t* coef;    // rebuild: block b's coefficient rows at coef + b*coef_bstride,
+  uint64_t coef_bstride;  //   coef_rows x kin bytes (tables built in LDS; tab unused)
+  uint32_t coef_rows;
   uint64_t n;             // blocks
   uint64_t tiles;         // tiles (= workgroups) of this segment
   uint64_t tiles_per_block;  // aligned mapping only
@@ -74,11 +79,11 @@ struct MacLaunch {
 struct DecodeArgs {
   const uint8_t* surv_idx;
   const uint8_t* lost_idx;
-  uint8_t* rows;          // n x e x k decode rows (optional)
-  uint32_t* tab;          // n x (R x kpad x 8) product-table images (optional)
+  uint8_t* rows;          // n x e x k decode rows
   uint32_t* status;
   uint64_t n;
-  uint32_t k, m, e, R, kpad;
+  uint32_t k, m, e;
+  uint32_t pitch;         // decode_coef_kernel: LDS row-staging pitch (set by the launcher)
 };
 
 struct Sha256Args {
@@ -109,9 +114,9 @@ int mac_rbound(int r);
 int mac_kchunk(int kin);
 void table_image_host(const uint8_t* coef, uint32_t r, uint32_t kin, uint32_t R, uint32_t kpad,
                       uint32_t* out);
-hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t lds,
+hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
                       hipStream_t st);
-hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st);
+hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st);  // closed-form decode rows
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);
 hipError_t launch_sha256(const Sha256Args& a, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);

@@ -3,7 +3,7 @@
 // Hot path: gf_mac_kernel, the batched GF(2^8) multiply-accumulate
 //   out[b][i][x] = XOR_j coef_b[i][j] * in[b][j][x]
 // which is RS encode (coef = the Cauchy parity rows, shared by every block)
-// and RS rebuild (coef = per-block decode rows from decode_rows_kernel).
+// and RS rebuild (coef = per-block decode rows from decode_coef_kernel).
 // It replaces the replication byte movement of Paxos::Details::
 // send_immutable_block / _fetch / _rebalance (src/memo/model/doughnut/
 // consensus/Paxos.cc:315-391, 486-519, 1012-1246); see DESIGN.md.
@@ -22,9 +22,11 @@
 //    ^ T_lo[x&3].  Each table has <= 8 byte entries, so one v_perm_b32 looks
 //    up 4 bytes at once: 3 perms + 1.5 v_bitop3_b32 (3-input XOR) per
 //    coefficient per dword; the field selectors are shared by all outputs.
-//  * The GF log/antilog tables live in LDS in decode_rows_kernel (batched
-//    Gauss-Jordan inversion), which also emits the per-block product-table
-//    images the rebuild MAC consumes.
+//  * Rebuild coefficients come from decode_coef_kernel: a closed-form
+//    (Cauchy/Lagrange) decode, one lane per block, with the GF log/antilog
+//    tables in LDS.  The MAC builds each block's product tables in LDS from
+//    its coefficient row (gf_xtime doublings), so per-block tables never
+//    travel through HBM.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -177,9 +179,12 @@ __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl
 template <int KC, int R>
 __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
                                           const uint32_t* tab, uint32_t kpad, uint32_t j0) {
+  // Pairing costs 12 selector VGPRs: the k = 16 body keeps 4 waves per
+  // SIMD only without it (MEMO_EC_MAC_PAIR16).
+  constexpr bool PAIR = MAC_PAIR && (KC != 16 || MEMO_EC_MAC_PAIR16);
 #pragma unroll
-  for (int g = 0; g < KC; g += MAC_PAIR ? 2 : 1) {
-    const bool two = MAC_PAIR && g + 1 < KC;
+  for (int g = 0; g < KC; g += PAIR ? 2 : 1) {
+    const bool two = PAIR && g + 1 < KC;
     Sel sa[4], sb[4];
     sa[0] = make_sel(d[g].x);
     sa[1] = make_sel(d[g].y);
@@ -331,15 +336,76 @@ __device__ __forceinline__ bool seg_tile(const MacLaunch& L, uint32_t& sid, uint
   return true;
 }
 
+// ---- Rebuild tables built in LDS from per-block decode coefficients.
+// Product-table image of coefficient c (the layout of table_dword), from its
+// doublings d_i = c * 2^i: lo = c*{0,1,2,3}, mid = c*{0..7}<<2,
+// hi = c*{0..7}<<5.
+__device__ __forceinline__ uint32_t gf_xtime(uint32_t x) { return (x << 1) ^ ((x >> 7) * 0x11Du); }
+__device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return a | (b << 8) | (c << 16) | (d << 24);
+}
+__device__ __forceinline__ void coef_image(uint32_t c, uint32_t* dst) {
+  const uint32_t d0 = c, d1 = gf_xtime(d0), d2 = gf_xtime(d1), d3 = gf_xtime(d2);
+  const uint32_t d4 = gf_xtime(d3), d5 = gf_xtime(d4), d6 = gf_xtime(d5), d7 = gf_xtime(d6);
+  const uint4 q = make_uint4(pack4(0, d2, d3, d2 ^ d3), pack4(d4, d4 ^ d2, d4 ^ d3, d4 ^ d3 ^ d2),
+                             pack4(0, d5, d6, d5 ^ d6), pack4(d7, d7 ^ d5, d7 ^ d6, d7 ^ d6 ^ d5));
+  *reinterpret_cast<uint4*>(dst) = q;
+  *reinterpret_cast<uint4*>(dst + 4) = make_uint4(pack4(0, d0, d1, d0 ^ d1), 0, 0, 0);
+}
+
+// Coefficient of table-image slot ci (set, row i, column j; kpad columns per
+// row, R rows per set): rows[b_first + set][i][j] for i < coef_rows, j < kin,
+// else 0 (padding).
+template <int R>
+__device__ __forceinline__ uint32_t coef_at(const MacSeg& sg, const Unit& u, uint32_t ci,
+                                            uint32_t kpad) {
+  const uint32_t set = ci / (R * kpad), rem = ci - set * (R * kpad);
+  const uint32_t i = rem / kpad, j = rem - i * kpad;
+  if (i >= sg.coef_rows || j >= sg.kin) return 0u;
+  return sg.coef[(u.b_first + set) * sg.coef_bstride + i * sg.kin + j];
+}
+
+// Register-staged coefficient loads for the hot path (issued before the
+// shard loads; vmcnt retires in order), then the images into LDS.
+template <int R, int KP>
+__device__ __forceinline__ void load_coefs(const MacSeg& sg, const Unit& u,
+                                           uint32_t (&cv)[MAC_COEF_REGS]) {
+  const uint32_t total = u.nsets * (R * KP);
+#pragma unroll
+  for (int q = 0; q < MAC_COEF_REGS; ++q) {
+    const uint32_t ci = threadIdx.x + 256u * q;
+    cv[q] = ci < total ? coef_at<R>(sg, u, ci, KP) : 0u;
+  }
+}
+template <int R, int KP>
+__device__ __forceinline__ void store_images(const Unit& u, const uint32_t (&cv)[MAC_COEF_REGS],
+                                             uint32_t* s_tab) {
+  const uint32_t total = u.nsets * (R * KP);
+#pragma unroll
+  for (int q = 0; q < MAC_COEF_REGS; ++q) {
+    const uint32_t ci = threadIdx.x + 256u * q;
+    if (ci < total) coef_image(cv[q], s_tab + ci * 8);
+  }
+}
+// Unstaged variant (generic chunk loop, runtime kpad).
+template <int R>
+__device__ __forceinline__ void stage_images(const MacSeg& sg, const Unit& u, uint32_t* s_tab) {
+  const uint32_t total = u.nsets * (R * sg.kpad);
+  for (uint32_t ci = threadIdx.x; ci < total; ci += 256)
+    coef_image(coef_at<R>(sg, u, ci, sg.kpad), s_tab + ci * 8);
+}
+
 // One tile of segment sg: KC is the straight-line shard chunk (kin == KC is
-// the hot path; other kin loop over chunks of KC shards).
-template <int KC, int R, bool NT>
+// the hot path; other kin loop over chunks of KC shards).  COEF: the tables
+// are built from per-block coefficient rows (rebuild), else copied from a
+// precomputed image (encode).
+template <int KC, int R, bool NT, bool COEF>
 __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32_t* s_tab) {
   const uint32_t kin = sg.kin, kpad = sg.kpad;
   const uint32_t set_dw = R * kpad * 8;
 
   const Unit u = locate(sg, tile);
-  const uint32_t* tab = s_tab + (sg.tab_bstride ? u.set * set_dw : 0u);
+  const uint32_t* tab = s_tab + ((COEF || sg.tab_bstride) ? u.set * set_dw : 0u);
   uint32_t acc[R][4];
 #pragma unroll
   for (int i = 0; i < R; ++i)
@@ -351,8 +417,9 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
     // order, so the LDS copy then waits only for them), the KC shard loads
     // right behind; the barrier and table copy overlap the shard loads.
 #if MEMO_EC_MAC_TABFIRST
-    uint32_t tv[MAC_TAB_REGS];
-    load_tables(sg, u, set_dw, tv);
+    uint32_t tv[COEF ? MAC_COEF_REGS : MAC_TAB_REGS];
+    if constexpr (COEF) load_coefs<R, KC>(sg, u, tv);
+    else load_tables(sg, u, set_dw, tv);
     uint4 d[KC];
 #if MEMO_EC_MAC_BUF
     const __amdgpu_buffer_rsrc_t rin = rsrc_of(sg.in + u.b_first * sg.in_bstride);
@@ -362,17 +429,20 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
 #pragma unroll
     for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
 #endif
-    store_tables(sg, u, set_dw, tv, s_tab);
+    if constexpr (COEF) store_images<R, KC>(u, tv, s_tab);
+    else store_tables(sg, u, set_dw, tv, s_tab);
 #else
     uint4 d[KC];
 #pragma unroll
     for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
-    stage_tables(sg, u, set_dw, s_tab);
+    if constexpr (COEF) stage_images<R>(sg, u, s_tab);
+    else stage_tables(sg, u, set_dw, s_tab);
 #endif
     __syncthreads();
     mac_chunk<KC, R>(acc, d, tab, kpad, 0);
   } else {
-    stage_tables(sg, u, set_dw, s_tab);
+    if constexpr (COEF) stage_images<R>(sg, u, s_tab);
+    else stage_tables(sg, u, set_dw, s_tab);
     __syncthreads();
     for (uint32_t j0 = 0; j0 < kin; j0 += KC) {
       uint4 d[KC];
@@ -401,246 +471,184 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   }
 }
 
-template <int KC, int R, bool NT>
-__global__ void __launch_bounds__(256, MEMO_EC_MAC_WAVES) gf_mac_kernel(const MacLaunch L) {
+// Minimum waves per SIMD asked of the register allocator: 1 leaves it free;
+// MEMO_EC_MAC_W16 pins the (16, R<=4) instances (132 VGPRs, 3 waves free).
+template <int KC, int R>
+constexpr int mac_min_waves() {
+  return (KC == 16 && R <= 4) ? MEMO_EC_MAC_W16 : 1;
+}
+
+template <int KC, int R, bool NT, bool COEF>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(mac_min_waves<KC, R>())))
+gf_mac_kernel(const MacLaunch L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
   uint32_t sid;
   uint64_t tile;
   if (!seg_tile(L, sid, tile)) return;
-  mac_tile<KC, R, NT>(L.seg[sid], tile, s_tab);
+  mac_tile<KC, R, NT, COEF>(L.seg[sid], tile, s_tab);
 }
 
-// ------------------------------------------------------------- decode rows
-// One wave per block: Gauss-Jordan on [A | I] in LDS, A = generator rows of
-// the k survivors; then rows_b[r] = C[lost[r]] * A^-1.  Lane l owns columns
-// l and l+64 of the augmented k x 2k matrix.  The field arithmetic uses the
-// LDS log/antilog image.  Optionally emits the block's product-table image
-// (R x kpad coefficients) for gf_mac_kernel.
-__device__ __forceinline__ uint32_t gen_entry(const uint8_t* lg, const uint8_t* ex, uint32_t k,
-                                              uint32_t s, uint32_t j) {
-  if (s < k) return s == j ? 1u : 0u;
-  return gf_inv_t(lg, ex, s ^ j);
+// ------------------------------------------------- closed-form decode rows
+// One LANE per block.  Every shard of the code is a scaled evaluation of
+// one polynomial: with f(z) = sum_j D_j / (z ^ j) over the k data indices
+// and F(z) = f(z) * prod_{j<k} (z ^ j) (degree < k), data shard j is
+// F(j) / sigma(j) and parity shard x is f(x) = F(x) / sigma(x), where
+// sigma(i) = prod_{j<k, j != i} (i ^ j) -- the Cauchy rows 1/(x ^ j) of the
+// generator.  The k survivors s_t are k evaluations of F, so Lagrange
+// interpolation gives every lost shard l directly:
+//   row_l[t] = W_t * Lam_l / (l ^ s_t),
+//   W_t   = sigma(s_t) / prod_{u != t} (s_t ^ s_u),
+//   Lam_l = prod_u (l ^ s_u) / sigma(l),
+// and row_l = unit vector when l is itself a survivor.  With
+// Pall(i) = prod_{j < k+m, j != i} (i ^ j) the survivor products become
+// products over the m non-survivors c (the complement):
+//   log W_t   = LW0(s_t) + sum_c log(s_t ^ c),
+//   log Lam_l = -LW0(l) - sum_{c != l} log(l ^ c),
+//   LW0(i)    = log sigma(i) - log Pall(i)   (per (k, m): LDS, per workgroup).
+// O(k*m + e*k) table lookups per block instead of a k x k Gauss-Jordan
+// elimination (round 1's decode_rows_reg_kernel: DESIGN.md 4.2).  Checked
+// against the oracle's
+// Gauss-Jordan rows (tests/test_gpu_parity.py).
+__device__ __forceinline__ uint32_t mod255(uint32_t x) {
+  x = (x & 0xFFu) + (x >> 8);
+  x = (x & 0xFFu) + (x >> 8);
+  return x >= 255u ? x - 255u : x;
 }
 
-__device__ __forceinline__ void wave_sync() {
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-}
-
-__global__ void __launch_bounds__(256) decode_rows_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_gf = smem;
+template <int KMAX>
+__global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_gf[192];
+  __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
+  __shared__ uint8_t s_comp[MEMO_EC_MAX_M][256];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch (staged rows)
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
   stage_gf(s_gf);
   __syncthreads();
-
-  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const uint64_t b = (uint64_t)blockIdx.x * 4 + wave;
-  if (b >= a.n) return;
-  const uint32_t k = a.k, e = a.e, total = a.k + a.m;
-  const uint32_t W = 2 * k;  // row width
-  uint8_t* base = reinterpret_cast<uint8_t*>(smem + 192);
-  uint8_t* M = base + wave * (MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K);
-  uint8_t* Rw = base + 4 * (MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K) + wave * (MEMO_EC_MAX_M * MEMO_EC_MAX_K);
-  const uint8_t* sidx = a.surv_idx + b * k;
-  const uint8_t* lidx = a.lost_idx + b * e;
-
-  bool bad = false;
-  // [A | I]
-  for (uint32_t r = 0; r < k; ++r) {
-    const uint32_t s = sidx[r];
-    bad |= s >= total;
-    for (uint32_t col = lane; col < W; col += 64) {
-      uint32_t v;
-      if (col < k) v = s < total ? gen_entry(lg, ex, k, s, col) : 0u;
-      else v = (col - k) == r ? 1u : 0u;
-      M[r * W + col] = (uint8_t)v;
+  const uint32_t k = a.k, m = a.m, e = a.e, nt = a.k + a.m;
+  for (uint32_t i = threadIdx.x; i < nt; i += 256) {
+    uint32_t ls = 0, lp = 0;
+    for (uint32_t j = 0; j < nt; ++j) {
+      if (j == i) continue;
+      const uint32_t v = lg[i ^ j];
+      lp += v;
+      if (j < k) ls += v;
     }
+    s_lw0[i] = mod255(mod255(ls) + 255u - mod255(lp));
   }
-  wave_sync();
-
-  for (uint32_t c = 0; c < k && !bad; ++c) {
-    // pivot: first row >= c with a nonzero entry in column c
-    const uint32_t pv = (lane < k && lane >= c) ? M[lane * W + c] : 0u;
-    const uint64_t mask = __ballot(pv != 0);
-    if (mask == 0) {
-      bad = true;
-      break;
-    }
-    const uint32_t p = (uint32_t)__builtin_ctzll(mask);
-    if (p != c) {
-      for (uint32_t col = lane; col < W; col += 64) {
-        const uint8_t t = M[c * W + col];
-        M[c * W + col] = M[p * W + col];
-        M[p * W + col] = t;
-      }
-      wave_sync();
-    }
-    const uint32_t iv = gf_inv_t(lg, ex, M[c * W + c]);
-    __builtin_amdgcn_wave_barrier();
-    for (uint32_t col = lane; col < W; col += 64)
-      M[c * W + col] = (uint8_t)gf_mul_t(lg, ex, iv, M[c * W + col]);
-    wave_sync();
-    for (uint32_t rr = 0; rr < k; ++rr) {
-      if (rr == c) continue;
-      const uint32_t f = M[rr * W + c];
-      wave_sync();
-      if (f) {
-        for (uint32_t col = lane; col < W; col += 64)
-          M[rr * W + col] ^= (uint8_t)gf_mul_t(lg, ex, f, M[c * W + col]);
-      }
-      wave_sync();
-    }
-  }
-
-  // rows[r][j] = XOR_t C[lost[r]][t] * Inv[t][j]; lane j (< k).
-  for (uint32_t r = 0; r < e; ++r) {
-    const uint32_t l = lidx[r];
-    const bool lbad = bad || l >= total;
-    if (lane < k) {
-      uint32_t acc = 0;
-      if (!lbad)
-        for (uint32_t t = 0; t < k; ++t)
-          acc ^= gf_mul_t(lg, ex, gen_entry(lg, ex, k, l, t), M[t * W + k + lane]);
-      Rw[r * k + lane] = (uint8_t)acc;
-    }
-    if (lbad) bad = true;
-  }
-  wave_sync();
-  if (bad) {  // invalid pattern: zero rows (zero output) + deferred error
-    for (uint32_t t = lane; t < e * k; t += 64) Rw[t] = 0;
-    wave_sync();
-    if (lane == 0 && a.status) atomicOr(a.status, 1u);
-  }
-  if (a.rows)
-    for (uint32_t t = lane; t < e * k; t += 64) a.rows[b * (uint64_t)e * k + t] = Rw[t];
-  if (a.tab) {
-    uint32_t* dst = a.tab + b * (uint64_t)a.R * a.kpad * 8;
-    const uint32_t n = a.R * a.kpad * 8;
-    for (uint32_t t = lane; t < n; t += 64) {
-      const uint32_t q = t & 7, cidx = t >> 3;
-      const uint32_t i = cidx / a.kpad, j = cidx - i * a.kpad;
-      const uint32_t c = (i < e && j < k) ? Rw[i * k + j] : 0u;
-      dst[t] = table_dword(lg, ex, c, q);
-    }
-  }
-}
-
-// Register-resident variant for k <= K (K in {4, 8, 10, 12, 16, 32}): lane l holds
-// column l of the K x 2K matrix [A | I] in VGPRs (A padded to K x K with an
-// identity block, whose inverse is the identity, so rows/columns >= k never
-// mix with the real ones).  Pivot rows and row factors are broadcast with
-// v_readlane; each elimination is one independent log/antilog LDS lookup per
-// row and lane (no LDS round trip of the matrix, no wave barriers).
-template <int K>
-__global__ void __launch_bounds__(256) decode_rows_reg_kernel(DecodeArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  uint32_t* s_gf = smem;
-  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
-  const uint8_t* ex = lg + 256;
-  stage_gf(s_gf);
   __syncthreads();
+  const uint32_t tid = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t b = b0 + tid;
+  const bool live = b < a.n;
+  const uint32_t ek = e * k;
+  // Rows are staged in LDS (pitch: an odd number of dwords, so the lanes'
+  // byte writes hit distinct banks) and leave as coalesced stores; rows too
+  // large for LDS go straight out.
+  const uint32_t pitch = a.pitch;
+  uint8_t* gout = a.rows + b * (uint64_t)ek;
+  uint8_t* out = pitch ? s_out + tid * pitch : gout;
 
-  const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const uint64_t b = (uint64_t)blockIdx.x * 4 + wave;
-  if (b >= a.n) return;
-  const uint32_t k = a.k, e = a.e, total = a.k + a.m;
-  uint8_t* Rw = reinterpret_cast<uint8_t*>(smem + 192) + wave * (MEMO_EC_MAX_M * MEMO_EC_MAX_K);
-  const uint8_t* sidx = a.surv_idx + b * k;
-  const uint8_t* lidx = a.lost_idx + b * e;
+  if (live) {
+    const uint8_t* sidx = a.surv_idx + b * k;
+    const uint8_t* lidx = a.lost_idx + b * e;
+    const bool dw = (k & 3) == 0 && (reinterpret_cast<uintptr_t>(a.surv_idx) & 3) == 0;
 
-  const bool left = lane < K;
-  const uint32_t col = left ? lane : lane - K;  // lanes >= 2K carry copies, unused
-  uint32_t m[K];
-  bool bad = false;
+    // survivors: indices, distinctness / range (bit set over k + m <= 80)
+    uint32_t sv[KMAX];
+    uint32_t mask[3] = {0u, 0u, 0u};
+    bool bad = false;
 #pragma unroll
-  for (int r = 0; r < K; ++r) {
-    if ((uint32_t)r < k) {
-      const uint32_t sv = sidx[r];
-      bad |= sv >= total;
-      if (left) m[r] = (col < k && sv < total) ? gen_entry(lg, ex, k, sv, col) : 0u;
-      else m[r] = col == (uint32_t)r ? 1u : 0u;
+    for (int t = 0; t < KMAX; ++t) {
+      sv[t] = 0;
+      if ((uint32_t)t < k) {
+        uint32_t v;
+        if (dw) v = (reinterpret_cast<const uint32_t*>(sidx)[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+        else v = sidx[t];
+        bad |= v >= nt;
+        const uint32_t w = (v >> 5) < 3 ? (v >> 5) : 2u, bit = 1u << (v & 31);
+        const uint32_t cur = w == 0 ? mask[0] : (w == 1 ? mask[1] : mask[2]);
+        bad |= (cur & bit) != 0;
+        if (w == 0) mask[0] |= bit;
+        else if (w == 1) mask[1] |= bit;
+        else mask[2] |= bit;
+        sv[t] = v;
+      }
+    }
+    auto is_surv = [&](uint32_t v) {
+      const uint32_t w = v >> 5, bit = 1u << (v & 31);
+      return ((w == 0 ? mask[0] : (w == 1 ? mask[1] : mask[2])) & bit) != 0;
+    };
+    // the m non-survivors
+    uint32_t cnt = 0;
+    for (uint32_t i = 0; i < nt; ++i)
+      if (!is_surv(i)) {
+        if (cnt < MEMO_EC_MAX_M) s_comp[cnt][tid] = (uint8_t)i;
+        ++cnt;
+      }
+    bad |= cnt != m;
+
+    // log W_t
+    uint32_t lw[KMAX];
+#pragma unroll
+    for (int t = 0; t < KMAX; ++t) lw[t] = ((uint32_t)t < k && !bad) ? s_lw0[sv[t]] : 0u;
+    if (!bad)
+      for (uint32_t c = 0; c < m; ++c) {
+        const uint32_t ci = s_comp[c][tid];
+#pragma unroll
+        for (int t = 0; t < KMAX; ++t)
+          if ((uint32_t)t < k) lw[t] += lg[sv[t] ^ ci];
+      }
+#pragma unroll
+    for (int t = 0; t < KMAX; ++t) lw[t] = mod255(lw[t]);
+
+    for (uint32_t r = 0; r < e; ++r) {
+      const uint32_t l = lidx[r];
+      bad |= l >= nt;
+      const bool unit = !bad && is_surv(l);
+      uint32_t llam = 0;  // log Lam_l
+      if (!bad && !unit) {
+        uint32_t acc = s_lw0[l];
+        for (uint32_t c = 0; c < m; ++c) {
+          const uint32_t ci = s_comp[c][tid];
+          if (ci != l) acc += lg[l ^ ci];
+        }
+        llam = 255u - mod255(acc);
+      }
+#pragma unroll
+      for (int t = 0; t < KMAX; ++t) {
+        if ((uint32_t)t < k) {
+          uint32_t v;
+          if (bad) v = 0;
+          else if (unit) v = sv[t] == l ? 1u : 0u;
+          else v = ex[mod255(lw[t] + llam + 255u - lg[l ^ sv[t]])];
+          out[r * k + t] = (uint8_t)v;
+        }
+      }
+    }
+    if (bad) {
+      for (uint32_t t = 0; t < ek; ++t) out[t] = 0;  // rows written before the fault
+      if (a.status) atomicOr(a.status, 1u);
+    }
+  }
+  if (pitch) {
+    __syncthreads();
+    // this workgroup's rows are one contiguous range of nb * ek bytes
+    const uint64_t nb = a.n - b0 < 256 ? a.n - b0 : 256;
+    uint8_t* dst = a.rows + b0 * ek;
+    const uint32_t total = (uint32_t)nb * ek;
+    if ((ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) {
+      const uint32_t ekw = ek >> 2;
+      for (uint32_t w = tid; w < (total >> 2); w += 256) {
+        const uint32_t lb = w / ekw, off = w - lb * ekw;
+        reinterpret_cast<uint32_t*>(dst)[w] =
+            *reinterpret_cast<const uint32_t*>(s_out + lb * pitch + off * 4);
+      }
     } else {
-      m[r] = col == (uint32_t)r ? 1u : 0u;  // identity padding, both halves
-    }
-  }
-
-#ifndef MEMO_EC_DECODE_DIAG_NOGJ  // diagnostic build: skip the elimination (wrong rows)
-#pragma unroll
-  for (int c = 0; c < K; ++c) {
-    if (bad) break;
-    // pivot: first row >= c with a nonzero entry in column c (lane c)
-    uint32_t pl = K;
-#pragma unroll
-    for (int r = K - 1; r >= c; --r)
-      if (m[r]) pl = r;
-    const uint32_t p = __builtin_amdgcn_readlane(pl, c);
-    if (p >= (uint32_t)K) {
-      bad = true;
-      break;
-    }
-    if (p != (uint32_t)c) {
-#pragma unroll
-      for (int r = c + 1; r < K; ++r)
-        if (p == (uint32_t)r) {
-          const uint32_t t = m[c];
-          m[c] = m[r];
-          m[r] = t;
-        }
-    }
-    const uint32_t piv = __builtin_amdgcn_readlane(m[c], c);
-    const uint32_t ilog = 255u - lg[piv];  // log of the pivot's inverse
-    const bool nz = m[c] != 0;
-    uint32_t lc = lg[m[c]] + ilog;          // log of the normalised entry
-    if (lc >= 255) lc -= 255;
-    m[c] = nz ? (uint32_t)ex[lc] : 0u;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-      if (r == c) continue;
-      const uint32_t f = __builtin_amdgcn_readlane(m[r], c);
-      if (f) m[r] ^= nz ? (uint32_t)ex[lc + lg[f]] : 0u;
-    }
-  }
-#endif
-
-  // Right half, lane K+j, now holds column j of A^-1: inv[t][j] = m[t].
-  for (uint32_t r = 0; r < e; ++r) {
-    const uint32_t l = lidx[r];
-    const bool lbad = bad || l >= total;
-    if (!left && col < k) {
-      uint32_t acc = 0;
-      if (!lbad) {
-        if (l < k) {
-#pragma unroll
-          for (int t = 0; t < K; ++t)
-            if ((uint32_t)t == l) acc = m[t];
-        } else {
-#pragma unroll
-          for (int t = 0; t < K; ++t)
-            if ((uint32_t)t < k) acc ^= gf_mul_t(lg, ex, gf_inv_t(lg, ex, l ^ (uint32_t)t), m[t]);
-        }
+      for (uint32_t x = tid; x < total; x += 256) {
+        const uint32_t lb = x / ek, off = x - lb * ek;
+        dst[x] = s_out[lb * pitch + off];
       }
-      Rw[r * k + col] = (uint8_t)acc;
-    }
-    if (lbad) bad = true;
-  }
-  wave_sync();
-  if (bad) {
-    for (uint32_t t = lane; t < e * k; t += 64) Rw[t] = 0;
-    wave_sync();
-    if (lane == 0 && a.status) atomicOr(a.status, 1u);
-  }
-  if (a.rows)
-    for (uint32_t t = lane; t < e * k; t += 64) a.rows[b * (uint64_t)e * k + t] = Rw[t];
-  if (a.tab) {
-    uint32_t* dst = a.tab + b * (uint64_t)a.R * a.kpad * 8;
-    const uint32_t n = a.R * a.kpad * 8;
-    for (uint32_t t = lane; t < n; t += 64) {
-      const uint32_t q = t & 7, cidx = t >> 3;
-      const uint32_t i = cidx / a.kpad, j = cidx - i * a.kpad;
-      const uint32_t c = (i < e && j < k) ? Rw[i * k + j] : 0u;
-      dst[t] = table_dword(lg, ex, c, q);
     }
   }
 }
@@ -836,17 +844,21 @@ hipError_t launch_sha256(const Sha256Args& a, hipStream_t st) {
 
 // ------------------------------------------------------------- launchers
 template <int KC, int R>
-static hipError_t launch_mac_t(const MacLaunch& L, uint32_t grid, size_t lds, hipStream_t st) {
-  hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
+static hipError_t launch_mac_t(bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+                               hipStream_t st) {
+  if (coef)
+    hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, true>), dim3(grid), dim3(256), lds, st, L);
+  else
+    hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, false>), dim3(grid), dim3(256), lds, st, L);
   return hipGetLastError();
 }
 
 template <int KC>
-static hipError_t launch_mac_r(int R, const MacLaunch& L, uint32_t grid, size_t lds,
+static hipError_t launch_mac_r(int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
                                hipStream_t st) {
   switch (R) {
 #define MEMO_EC_R(x) \
-  case x: return launch_mac_t<KC, x>(L, grid, lds, st);
+  case x: return launch_mac_t<KC, x>(coef, L, grid, lds, st);
     MEMO_EC_R(1) MEMO_EC_R(2) MEMO_EC_R(3) MEMO_EC_R(4) MEMO_EC_R(6) MEMO_EC_R(8)
     MEMO_EC_R(12) MEMO_EC_R(16)
 #undef MEMO_EC_R
@@ -869,41 +881,41 @@ int mac_kchunk(int kin) {
   }
 }
 
-hipError_t launch_mac(int KC, int R, const MacLaunch& L, uint32_t grid, size_t lds,
+hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
                       hipStream_t st) {
   switch (KC) {
-    case 2: return launch_mac_r<2>(R, L, grid, lds, st);
-    case 3: return launch_mac_r<3>(R, L, grid, lds, st);
-    case 4: return launch_mac_r<4>(R, L, grid, lds, st);
-    case 10: return launch_mac_r<10>(R, L, grid, lds, st);
-    case 16: return launch_mac_r<16>(R, L, grid, lds, st);
+    case 2: return launch_mac_r<2>(R, coef, L, grid, lds, st);
+    case 3: return launch_mac_r<3>(R, coef, L, grid, lds, st);
+    case 4: return launch_mac_r<4>(R, coef, L, grid, lds, st);
+    case 10: return launch_mac_r<10>(R, coef, L, grid, lds, st);
+    case 16: return launch_mac_r<16>(R, coef, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_decode_rows(const DecodeArgs& a, hipStream_t st) {
-  const uint32_t grid = (uint32_t)((a.n + 3) / 4);
+hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
+  DecodeArgs a = a0;
+  const uint32_t grid = (uint32_t)((a.n + 255) / 256);
   if (grid == 0) return hipSuccess;
-  const size_t lds_reg = 768 + 4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
-  if (a.k <= 4 && !MEMO_EC_DECODE_LDS) {
-    hipLaunchKernelGGL(decode_rows_reg_kernel<4>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else if (a.k <= 8 && !MEMO_EC_DECODE_LDS) {
-    hipLaunchKernelGGL(decode_rows_reg_kernel<8>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else if (a.k <= 10 && !MEMO_EC_DECODE_LDS) {  // RS(10,m): no padding steps
-    hipLaunchKernelGGL(decode_rows_reg_kernel<10>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else if (a.k <= 12 && !MEMO_EC_DECODE_LDS) {
-    hipLaunchKernelGGL(decode_rows_reg_kernel<12>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else if (a.k <= 16 && !MEMO_EC_DECODE_LDS) {
-    hipLaunchKernelGGL(decode_rows_reg_kernel<16>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else if (a.k <= 32 && !MEMO_EC_DECODE_LDS) {
-    hipLaunchKernelGGL(decode_rows_reg_kernel<32>, dim3(grid), dim3(256), lds_reg, st, a);
-  } else {
-    const size_t lds = 768 + 4 * (size_t)MEMO_EC_MAX_K * 2 * MEMO_EC_MAX_K +
-                       4 * (size_t)MEMO_EC_MAX_M * MEMO_EC_MAX_K;
-    hipLaunchKernelGGL(decode_rows_kernel, dim3(grid), dim3(256), lds, st, a);
-  }
+  // LDS staging of the rows: pitch = e*k rounded up to an odd dword count
+  const uint32_t ek = a.e * a.k;
+  uint32_t pw = (ek + 3) / 4;
+  pw |= 1u;
+  a.pitch = 256u * pw * 4 <= 64 * 1024 ? pw * 4 : 0u;
+  const size_t lds = a.pitch ? 256u * a.pitch : 0;
+  if (a.k <= 4)
+    hipLaunchKernelGGL(decode_coef_kernel<4>, dim3(grid), dim3(256), lds, st, a);
+  else if (a.k <= 10)
+    hipLaunchKernelGGL(decode_coef_kernel<10>, dim3(grid), dim3(256), lds, st, a);
+  else if (a.k <= 16)
+    hipLaunchKernelGGL(decode_coef_kernel<16>, dim3(grid), dim3(256), lds, st, a);
+  else if (a.k <= 32)
+    hipLaunchKernelGGL(decode_coef_kernel<32>, dim3(grid), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL(decode_coef_kernel<64>, dim3(grid), dim3(256), lds, st, a);
   return hipGetLastError();
 }
+
 
 hipError_t launch_fill(const FillArgs& a, hipStream_t st) {
   const uint64_t total = a.n * (a.stride / 16);

@@ -85,7 +85,8 @@ int check_km(int k, int m) {
 struct Plan {
   MacSeg seg{};
   int KC = 4, R = 1;
-  size_t lds = 0;  // LDS bytes of this segment's table sets
+  bool coef = false;  // tables built from per-block coefficient rows (rebuild)
+  size_t lds = 0;     // LDS bytes of this segment's table sets
 };
 
 uint32_t kpad_of(uint32_t kin, int KC) { return (kin + KC - 1) / KC * KC; }
@@ -95,21 +96,24 @@ uint64_t sets_per_tile(uint64_t C) { return (MAC_TILE - 1 + C - 1) / C + 1; }
 
 Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* in,
                   uint64_t in_bs, uint64_t in_ss, uint8_t* out, uint64_t out_bs, uint64_t out_ss,
-                  const uint32_t* tab, uint64_t tab_bs_dw, int KC, int R) {
+                  const uint32_t* tab, uint64_t tab_bs_dw, int KC, int R,
+                  const uint8_t* coef = nullptr, uint64_t coef_bs = 0, uint32_t coef_rows = 0) {
   Plan p;
   p.KC = KC;
   p.R = R;
+  p.coef = coef != nullptr;
   MacSeg& s = p.seg;
   s.in = in; s.out = out; s.tab = tab;
   s.in_bstride = in_bs; s.in_sstride = in_ss;
   s.out_bstride = out_bs; s.out_sstride = out_ss;
   s.tab_bstride = tab_bs_dw;
+  s.coef = coef; s.coef_bstride = coef_bs; s.coef_rows = coef_rows;
   s.n = n; s.kin = kin; s.r = r;
   s.kpad = kpad_of(kin, KC);
   s.chunks = (uint32_t)(S / 16);
   const size_t set_bytes = (size_t)R * s.kpad * 32;
   const uint64_t C = s.chunks;
-  if (tab_bs_dw == 0) {  // one image for every block
+  if (tab_bs_dw == 0 && !coef) {  // one image for every block
     s.flat = 1;
     p.lds = set_bytes;
   } else if (sets_per_tile(C) * set_bytes <= kLdsBudget) {
@@ -155,8 +159,9 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   uint64_t wg = 0;
   size_t lds = 0;
   const int KC = plans[0].KC, R = plans[0].R;
+  const bool coef = plans[0].coef;
   for (auto& p : plans) {
-    if (p.KC != KC || p.R != R) return MEMO_EC_EINVAL;
+    if (p.KC != KC || p.R != R || p.coef != coef) return MEMO_EC_EINVAL;
     if (p.seg.tiles == 0) continue;
     wg = (wg + 7) / 8 * 8;  // segments start on an XCD-round boundary
     p.seg.wg_begin = (uint32_t)wg;
@@ -172,7 +177,7 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   for (uint32_t i = 0; i < L.nseg; ++i) min_tiles = std::min<uint64_t>(min_tiles, L.seg[i].tiles);
   L.xcd = min_tiles >= xcd_min_tiles() ? 1u : 0u;
   if (lds > 160 * 1024) return MEMO_EC_ERANGE;
-  return hip_rc(launch_mac(KC, R, L, (uint32_t)wg, lds, st));
+  return hip_rc(launch_mac(KC, R, coef, L, (uint32_t)wg, lds, st));
 }
 
 // Cached device table image of the Cauchy parity rows of (k, m).
@@ -301,33 +306,33 @@ int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint
   return MEMO_EC_OK;
 }
 
-// Device-resident rebuild on stream st: decode rows (+ per-block table
-// images) then the MAC.  `rows` may be null; `tabs` has room for n images.
+// Device-resident rebuild on stream st: closed-form decode rows (one lane per
+// block), then the MAC, which builds each block's product tables in LDS from
+// its rows.  `scratch` has room for tab_bytes(k, e, n).
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
-                   uint8_t* rows, uint32_t* tabs, hipStream_t st) {
+                   void* scratch, hipStream_t st) {
   const int KC = mac_kchunk(k), R = mac_rbound(e);
-  const uint32_t kpad = kpad_of((uint32_t)k, KC);
-  const uint64_t img_dw = (uint64_t)R * kpad * 8;
-  DecodeArgs a{surv_idx, lost_idx, rows, tabs, ctx->d_status, n, (uint32_t)k, (uint32_t)m,
-               (uint32_t)e, (uint32_t)R, kpad};
-  HIPCHK(launch_decode_rows(a, st));
   const size_t step = max_blocks_per_launch(S);
+  uint8_t* rows = static_cast<uint8_t*>(scratch);
+  const uint64_t row_b = (uint64_t)e * k;
+  DecodeArgs a{surv_idx, lost_idx, rows, ctx->d_status, n, (uint32_t)k, (uint32_t)m,
+               (uint32_t)e, 0};
+  HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
     std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, cnt,
                                          surv + b0 * (size_t)k * S, (uint64_t)k * S, S,
                                          out + b0 * (size_t)e * S, (uint64_t)e * S, S,
-                                         tabs + b0 * img_dw, img_dw, KC, R)};
+                                         nullptr, 0, KC, R, rows + b0 * row_b, row_b,
+                                         (uint32_t)e)};
     if (int rc = launch_plans(plans, st)) return rc;
   }
   return MEMO_EC_OK;
 }
 
-size_t tab_bytes(int k, int e, size_t n) {
-  const int KC = mac_kchunk(k), R = mac_rbound(e);
-  return n * (size_t)R * kpad_of((uint32_t)k, KC) * 32;
-}
+// Rebuild scratch for n blocks: their decode rows, e x k bytes each.
+size_t tab_bytes(int k, int e, size_t n) { return n * (size_t)e * k; }
 
 // Host-memory pipeline over batches of nb blocks.  Batch i uses slot i % 3:
 //   in(slot, b0, cnt, st)   host staging + HtoD copies on st
@@ -551,9 +556,8 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   if (n == 0 || e == 0) return MEMO_EC_OK;
   if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
-  DecodeArgs a{surv_idx, lost_idx, rows, nullptr, c->d_status, n, (uint32_t)k, (uint32_t)m,
-               (uint32_t)e, 0, 0};
-  return hip_rc(launch_decode_rows(a, c->stream));
+  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0};
+  return hip_rc(launch_decode_coef(a, c->stream));
 }
 
 int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
@@ -567,8 +571,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   DeviceGuard g(c->device);
   if (where == MEMO_EC_DEVICE) {
     if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
-    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, nullptr, c->d_tabs,
-                          c->stream);
+    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_tabs, c->stream);
   }
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
@@ -600,8 +603,8 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       },
       [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
         uint8_t* d = c->d_slot[s];
-        return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out, nullptr,
-                              c->d_tabs + (size_t)s * tabs / 4, st);
+        return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out,
+                              reinterpret_cast<uint8_t*>(c->d_tabs) + (size_t)s * tabs, st);
       },
       [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + o_out;

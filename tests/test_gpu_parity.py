@@ -156,6 +156,27 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m):
     assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost))
 
 
+@pytest.mark.parametrize("k,m", [(1, 1), (3, 2), (4, 2), (7, 5), (10, 4), (16, 4), (20, 8),
+                                 (33, 12), (64, 16)])
+def test_decode_rows_vs_oracle(codec, O, k, m):
+    """Closed-form decode rows (decode_coef_kernel, one lane per block)
+    against the oracle's Gauss-Jordan rows C[lost] * inv(C[surv]): random
+    survivor orders, lost shards that are data, parity or themselves
+    survivors (unit rows), e = 1..m, over 700 blocks (several workgroups)."""
+    rng = np.random.default_rng(k * 1000 + m)
+    n = 700
+    for e in sorted({1, (m + 1) // 2, m}):
+        surv = np.stack([rng.permutation(k + m)[:k] for _ in range(n)]).astype(np.uint8)
+        lost = np.stack([rng.permutation(k + m)[:e] for _ in range(n)]).astype(np.uint8)
+        rows = empty(n, e * k)
+        codec.decode_rows(k, m, dev(surv), dev(lost), rows)
+        codec.synchronize()
+        got = host(rows).reshape(n, e, k)
+        for b in range(0, n, 7):
+            want = O.decode_matrix(k, m, surv[b], lost[b])
+            assert np.array_equal(got[b], want), (k, m, e, b)
+
+
 def test_small_blocks_many_per_tile(codec, O):
     # 4 KiB blocks with k=16: S=256, 16 columns per block, tables for ~17
     # blocks per tile in the rebuild kernel.
