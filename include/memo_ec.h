@@ -119,9 +119,13 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
                           const uint8_t *lost_idx, int e, uint8_t *out,
                           int where);
 
-/* Per-block decode rows (n x e x k bytes, device) -- the batched GF(2^8)
- * inversion that memo_ec_rebuild_batch runs before its multiply-accumulate.
- * Device pointers only; asynchronous on the ctx stream. */
+/* Per-block decode rows (n x e x k bytes, device): row r of block b holds the
+ * coefficients of lost_idx[b][r] over the survivors in surv_idx[b] order,
+ * i.e. C[lost] * inv(C[surv]) -- computed in closed form (one lane per block,
+ * no matrix inversion), as memo_ec_rebuild_batch does before its
+ * multiply-accumulate.  Device pointers only; asynchronous on the ctx
+ * stream; invalid survivor sets give zero rows and MEMO_EC_ESINGULAR at
+ * memo_ec_synchronize. */
 int memo_ec_decode_rows(memo_ec_ctx *ctx, int k, int m, size_t n,
                         const uint8_t *surv_idx, const uint8_t *lost_idx,
                         int e, uint8_t *rows);
