@@ -32,6 +32,7 @@
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif
+
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
 #endif
@@ -59,7 +60,8 @@ struct MacSeg {
   uint64_t out_bstride, out_sstride;
   uint64_t tab_bstride;   // dwords between blocks' images; 0 = one image for all
   const uint8_t* coef;    // rebuild: block b's coefficient rows at coef + b*coef_bstride,
-  uint64_t coef_bstride;  //   coef_rows x kin bytes (tables built in LDS; tab unused)
+  uint64_t coef_bstride;  //   coef_rows x kin bytes (tables built in LDS; tab unused);
+                          //   coef_bstride 0: one set of rows for every block
   uint32_t coef_rows;
   uint64_t n;             // blocks
   uint64_t tiles;         // tiles (= workgroups) of this segment

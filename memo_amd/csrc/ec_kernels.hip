@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "ec_kernels.h"
 
 namespace memo_ec {
@@ -365,12 +367,18 @@ __device__ __forceinline__ uint32_t coef_at(const MacSeg& sg, const Unit& u, uin
   return sg.coef[(u.b_first + set) * sg.coef_bstride + i * sg.kin + j];
 }
 
+// Table sets a tile builds: one per block, or one for all when the
+// coefficients are shared (coef_bstride 0: encode's parity rows).
+__device__ __forceinline__ uint32_t coef_sets(const MacSeg& sg, const Unit& u) {
+  return sg.coef_bstride ? u.nsets : 1u;
+}
+
 // Register-staged coefficient loads for the hot path (issued before the
 // shard loads; vmcnt retires in order), then the images into LDS.
 template <int R, int KP>
 __device__ __forceinline__ void load_coefs(const MacSeg& sg, const Unit& u,
                                            uint32_t (&cv)[MAC_COEF_REGS]) {
-  const uint32_t total = u.nsets * (R * KP);
+  const uint32_t total = coef_sets(sg, u) * (R * KP);
 #pragma unroll
   for (int q = 0; q < MAC_COEF_REGS; ++q) {
     const uint32_t ci = threadIdx.x + 256u * q;
@@ -378,9 +386,9 @@ __device__ __forceinline__ void load_coefs(const MacSeg& sg, const Unit& u,
   }
 }
 template <int R, int KP>
-__device__ __forceinline__ void store_images(const Unit& u, const uint32_t (&cv)[MAC_COEF_REGS],
-                                             uint32_t* s_tab) {
-  const uint32_t total = u.nsets * (R * KP);
+__device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
+                                             const uint32_t (&cv)[MAC_COEF_REGS], uint32_t* s_tab) {
+  const uint32_t total = coef_sets(sg, u) * (R * KP);
 #pragma unroll
   for (int q = 0; q < MAC_COEF_REGS; ++q) {
     const uint32_t ci = threadIdx.x + 256u * q;
@@ -390,7 +398,7 @@ __device__ __forceinline__ void store_images(const Unit& u, const uint32_t (&cv)
 // Unstaged variant (generic chunk loop, runtime kpad).
 template <int R>
 __device__ __forceinline__ void stage_images(const MacSeg& sg, const Unit& u, uint32_t* s_tab) {
-  const uint32_t total = u.nsets * (R * sg.kpad);
+  const uint32_t total = coef_sets(sg, u) * (R * sg.kpad);
   for (uint32_t ci = threadIdx.x; ci < total; ci += 256)
     coef_image(coef_at<R>(sg, u, ci, sg.kpad), s_tab + ci * 8);
 }
@@ -405,7 +413,8 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   const uint32_t set_dw = R * kpad * 8;
 
   const Unit u = locate(sg, tile);
-  const uint32_t* tab = s_tab + ((COEF || sg.tab_bstride) ? u.set * set_dw : 0u);
+  const bool per_block = COEF ? sg.coef_bstride != 0 : sg.tab_bstride != 0;
+  const uint32_t* tab = s_tab + (per_block ? u.set * set_dw : 0u);
   uint32_t acc[R][4];
 #pragma unroll
   for (int i = 0; i < R; ++i)
@@ -429,7 +438,7 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
 #pragma unroll
     for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
 #endif
-    if constexpr (COEF) store_images<R, KC>(u, tv, s_tab);
+    if constexpr (COEF) store_images<R, KC>(sg, u, tv, s_tab);
     else store_tables(sg, u, set_dw, tv, s_tab);
 #else
     uint4 d[KC];
@@ -515,6 +524,21 @@ __device__ __forceinline__ uint32_t mod255(uint32_t x) {
   return x >= 255u ? x - 255u : x;
 }
 
+// LW0(i) = log sigma(i) - log Pall(i) for i < k + m, into LDS.
+__device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_t nt,
+                                          uint32_t* s_lw0) {
+  for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
+    uint32_t ls = 0, lp = 0;
+    for (uint32_t j = 0; j < nt; ++j) {
+      if (j == i) continue;
+      const uint32_t v = lg[i ^ j];
+      lp += v;
+      if (j < k) ls += v;
+    }
+    s_lw0[i] = mod255(mod255(ls) + 255u - mod255(lp));
+  }
+}
+
 template <int KMAX>
 __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t s_gf[192];
@@ -526,16 +550,7 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   stage_gf(s_gf);
   __syncthreads();
   const uint32_t k = a.k, m = a.m, e = a.e, nt = a.k + a.m;
-  for (uint32_t i = threadIdx.x; i < nt; i += 256) {
-    uint32_t ls = 0, lp = 0;
-    for (uint32_t j = 0; j < nt; ++j) {
-      if (j == i) continue;
-      const uint32_t v = lg[i ^ j];
-      lp += v;
-      if (j < k) ls += v;
-    }
-    s_lw0[i] = mod255(mod255(ls) + 255u - mod255(lp));
-  }
+  stage_lw0(lg, k, nt, s_lw0);
   __syncthreads();
   const uint32_t tid = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * 256;
@@ -650,6 +665,84 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
         dst[x] = s_out[lb * pitch + off];
       }
     }
+  }
+}
+
+// Latency variant for small batches: L lanes per block (L = the power of two
+// >= k), lane t owns survivor column t.  The block's survivor bit set is
+// OR-reduced across its L lanes; each lane then needs only its own W_t
+// (m lookups) and, per lost shard, Lam_l (m lookups) and one coefficient.
+// About k + m + e * (k + m + 2) lookups per lane against the per-block
+// kernel's k * m + e * (m + 2k) in one lane: a few microseconds for a
+// C3-sized batch instead of ~15.
+template <int L>
+__global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_gf[192];
+  __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
+  const uint8_t* ex = lg + 256;
+  stage_gf(s_gf);
+  __syncthreads();
+  const uint32_t k = a.k, e = a.e, nt = a.k + a.m, ek = a.e * a.k;
+  stage_lw0(lg, k, nt, s_lw0);
+  __syncthreads();
+  const uint32_t t = threadIdx.x % L;
+  const uint64_t b = (uint64_t)blockIdx.x * (256 / L) + threadIdx.x / L;
+  if (b >= a.n) return;  // whole groups; no barrier below
+  const bool col = t < k;
+  const uint32_t sv = col ? a.surv_idx[b * k + t] : 0u;
+  bool bad = col && sv >= nt;
+  uint32_t mk[3] = {0u, 0u, 0u};
+  if (col && sv < nt) {
+    const uint32_t w = sv >> 5, bit = 1u << (sv & 31);
+    if (w == 0) mk[0] = bit;
+    else if (w == 1) mk[1] = bit;
+    else mk[2] = bit;
+  }
+  uint32_t badw = bad ? 1u : 0u;
+#pragma unroll
+  for (int off = 1; off < L; off <<= 1) {
+    mk[0] |= __shfl_xor(mk[0], off, L);
+    mk[1] |= __shfl_xor(mk[1], off, L);
+    mk[2] |= __shfl_xor(mk[2], off, L);
+    badw |= __shfl_xor(badw, off, L);
+  }
+  // out of range anywhere, or duplicates (fewer than k distinct bits)
+  bad = badw != 0 || (uint32_t)(__popc(mk[0]) + __popc(mk[1]) + __popc(mk[2])) != k;
+  auto is_surv = [&](uint32_t v) {
+    const uint32_t w = v >> 5, bit = 1u << (v & 31);
+    return ((w == 0 ? mk[0] : (w == 1 ? mk[1] : mk[2])) & bit) != 0;
+  };
+  uint32_t lw = 0;  // log W_t
+  if (col && !bad) {
+    lw = s_lw0[sv];
+    for (uint32_t i = 0; i < nt; ++i)
+      if (!is_surv(i)) lw += lg[sv ^ i];
+    lw = mod255(lw);
+  }
+  uint8_t* out = a.rows + b * (uint64_t)ek;
+  for (uint32_t r = 0; r < e; ++r) {
+    const uint32_t l = a.lost_idx[b * e + r];  // the same for the whole group
+    bad |= l >= nt;
+    const bool unit = !bad && is_surv(l);
+    uint32_t llam = 0;  // log Lam_l
+    if (!bad && !unit) {
+      uint32_t acc = s_lw0[l];
+      for (uint32_t i = 0; i < nt; ++i)
+        if (!is_surv(i) && i != l) acc += lg[l ^ i];
+      llam = 255u - mod255(acc);
+    }
+    if (col) {
+      uint32_t v;
+      if (bad) v = 0;
+      else if (unit) v = sv == l ? 1u : 0u;
+      else v = ex[mod255(lw + llam + 255u - lg[l ^ sv])];
+      out[r * k + t] = (uint8_t)v;
+    }
+  }
+  if (bad) {  // the group's lanes share one wave: these stores follow the row stores
+    for (uint32_t x = t; x < ek; x += L) out[x] = 0;
+    if (t == 0 && a.status) atomicOr(a.status, 1u);
   }
 }
 
@@ -893,10 +986,30 @@ hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t gri
   }
 }
 
+// Largest batch that takes the column-per-lane decode (MEMO_EC_DECODE_WIDE_MAX
+// overrides, read per call: tuning and tests).
+static uint64_t decode_wide_max_blocks() {
+  const char* p = std::getenv("MEMO_EC_DECODE_WIDE_MAX");
+  return p ? std::strtoull(p, nullptr, 10) : (uint64_t)65536;
+}
+
 hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   DecodeArgs a = a0;
+  if (a.n == 0) return hipSuccess;
+  // Small batches are latency-bound: one lane per survivor column.
+  if (a.n <= decode_wide_max_blocks()) {
+    const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
+    const uint32_t g = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
+    switch (L) {
+      case 4: hipLaunchKernelGGL(decode_coef_wide_kernel<4>, dim3(g), dim3(256), 0, st, a); break;
+      case 8: hipLaunchKernelGGL(decode_coef_wide_kernel<8>, dim3(g), dim3(256), 0, st, a); break;
+      case 16: hipLaunchKernelGGL(decode_coef_wide_kernel<16>, dim3(g), dim3(256), 0, st, a); break;
+      case 32: hipLaunchKernelGGL(decode_coef_wide_kernel<32>, dim3(g), dim3(256), 0, st, a); break;
+      default: hipLaunchKernelGGL(decode_coef_wide_kernel<64>, dim3(g), dim3(256), 0, st, a); break;
+    }
+    return hipGetLastError();
+  }
   const uint32_t grid = (uint32_t)((a.n + 255) / 256);
-  if (grid == 0) return hipSuccess;
   // LDS staging of the rows: pitch = e*k rounded up to an odd dword count
   const uint32_t ek = a.e * a.k;
   uint32_t pw = (ek + 3) / 4;

@@ -113,7 +113,7 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   s.chunks = (uint32_t)(S / 16);
   const size_t set_bytes = (size_t)R * s.kpad * 32;
   const uint64_t C = s.chunks;
-  if (tab_bs_dw == 0 && !coef) {  // one image for every block
+  if (coef ? coef_bs == 0 : tab_bs_dw == 0) {  // one table set for every block
     s.flat = 1;
     p.lds = set_bytes;
   } else if (sets_per_tile(C) * set_bytes <= kLdsBudget) {

@@ -158,11 +158,16 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m):
 
 @pytest.mark.parametrize("k,m", [(1, 1), (3, 2), (4, 2), (7, 5), (10, 4), (16, 4), (20, 8),
                                  (33, 12), (64, 16)])
-def test_decode_rows_vs_oracle(codec, O, k, m):
-    """Closed-form decode rows (decode_coef_kernel, one lane per block)
-    against the oracle's Gauss-Jordan rows C[lost] * inv(C[surv]): random
-    survivor orders, lost shards that are data, parity or themselves
-    survivors (unit rows), e = 1..m, over 700 blocks (several workgroups)."""
+@pytest.mark.parametrize("kernel", ["wide", "per_block"])
+def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
+    """Closed-form decode rows against the oracle's Gauss-Jordan rows
+    C[lost] * inv(C[surv]): random survivor orders, lost shards that are
+    data, parity or themselves survivors (unit rows), e = 1..m, over 700
+    blocks (several workgroups).  Both kernels: column-per-lane
+    (decode_coef_wide_kernel, small batches) and one lane per block
+    (decode_coef_kernel, forced by MEMO_EC_DECODE_WIDE_MAX=0)."""
+    if kernel == "per_block":
+        monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
     rng = np.random.default_rng(k * 1000 + m)
     n = 700
     for e in sorted({1, (m + 1) // 2, m}):
@@ -261,6 +266,30 @@ def test_singular_survivors_reported(codec):
         codec.synchronize()
     assert ei.value.code == -4
     codec.synchronize()  # error is cleared
+
+
+@pytest.mark.parametrize("kernel", ["wide", "per_block"])
+def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
+    """Duplicate survivors, a survivor index >= k+m and a lost index >= k+m
+    zero that block's rows (only that block's) and raise ESINGULAR once."""
+    from memo_amd import ec
+    if kernel == "per_block":
+        monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
+    k, m, e = 10, 4, 2
+    surv = np.array([list(range(10)), [0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [0, 1, 2, 3, 4, 5, 6, 7, 8, 14],
+                     [13, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(10))], np.uint8)
+    lost = np.array([[10, 11], [10, 11], [10, 11], [0, 12], [11, 14]], np.uint8)
+    rows = empty(5, e * k)
+    codec.decode_rows(k, m, dev(surv), dev(lost), rows)
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.synchronize()
+    assert ei.value.code == -4
+    got = host(rows).reshape(5, e, k)
+    for b in (1, 2, 4):
+        assert not got[b].any(), b
+    for b in (0, 3):
+        assert np.array_equal(got[b], O.decode_matrix(k, m, surv[b], lost[b])), b
+    codec.synchronize()
 
 
 def test_singular_survivors_reported_host_paths(codec, O, monkeypatch):
