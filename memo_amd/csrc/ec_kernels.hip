@@ -527,13 +527,15 @@ __device__ __forceinline__ uint32_t mod255(uint32_t x) {
 // LW0(i) = log sigma(i) - log Pall(i) for i < k + m, into LDS.
 __device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_t nt,
                                           uint32_t* s_lw0) {
+  // j == i adds log[0] = 0; the lookups are branch-free so that the unrolled
+  // loop keeps several LDS reads in flight
   for (uint32_t i = threadIdx.x; i < nt; i += blockDim.x) {
     uint32_t ls = 0, lp = 0;
+#pragma unroll 8
     for (uint32_t j = 0; j < nt; ++j) {
-      if (j == i) continue;
       const uint32_t v = lg[i ^ j];
       lp += v;
-      if (j < k) ls += v;
+      ls += j < k ? v : 0u;
     }
     s_lw0[i] = mod255(mod255(ls) + 255u - mod255(lp));
   }
@@ -547,15 +549,33 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch (staged rows)
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
-  stage_gf(s_gf);
-  __syncthreads();
   const uint32_t k = a.k, m = a.m, e = a.e, nt = a.k + a.m;
-  stage_lw0(lg, k, nt, s_lw0);
-  __syncthreads();
   const uint32_t tid = threadIdx.x;
   const uint64_t b0 = (uint64_t)blockIdx.x * 256;
   const uint64_t b = b0 + tid;
   const bool live = b < a.n;
+  // The block's indices are loaded first, so their latency overlaps the
+  // table staging.
+  uint32_t sv[KMAX];
+  {
+    const uint8_t* sidx = a.surv_idx + b * k;
+    const bool dw = (k & 3) == 0 && (reinterpret_cast<uintptr_t>(a.surv_idx) & 3) == 0;
+#pragma unroll
+    for (int t = 0; t < KMAX; ++t) {
+      sv[t] = 0;
+      if (live && (uint32_t)t < k) {
+        if (dw) sv[t] = (reinterpret_cast<const uint32_t*>(sidx)[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+        else sv[t] = sidx[t];
+      }
+    }
+  }
+  uint32_t lv[MEMO_EC_MAX_M];
+#pragma unroll
+  for (int r = 0; r < MEMO_EC_MAX_M; ++r) lv[r] = (live && (uint32_t)r < e) ? a.lost_idx[b * e + r] : 0u;
+  stage_gf(s_gf);
+  __syncthreads();
+  stage_lw0(lg, k, nt, s_lw0);
+  __syncthreads();
   const uint32_t ek = e * k;
   // Rows are staged in LDS (pitch: an odd number of dwords, so the lanes'
   // byte writes hit distinct banks) and leave as coalesced stores; rows too
@@ -565,21 +585,13 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   uint8_t* out = pitch ? s_out + tid * pitch : gout;
 
   if (live) {
-    const uint8_t* sidx = a.surv_idx + b * k;
-    const uint8_t* lidx = a.lost_idx + b * e;
-    const bool dw = (k & 3) == 0 && (reinterpret_cast<uintptr_t>(a.surv_idx) & 3) == 0;
-
-    // survivors: indices, distinctness / range (bit set over k + m <= 80)
-    uint32_t sv[KMAX];
+    // survivors: distinctness / range (bit set over k + m <= 80)
     uint32_t mask[3] = {0u, 0u, 0u};
     bool bad = false;
 #pragma unroll
     for (int t = 0; t < KMAX; ++t) {
-      sv[t] = 0;
       if ((uint32_t)t < k) {
-        uint32_t v;
-        if (dw) v = (reinterpret_cast<const uint32_t*>(sidx)[t >> 2] >> (8 * (t & 3))) & 0xFFu;
-        else v = sidx[t];
+        const uint32_t v = sv[t];
         bad |= v >= nt;
         const uint32_t w = (v >> 5) < 3 ? (v >> 5) : 2u, bit = 1u << (v & 31);
         const uint32_t cur = w == 0 ? mask[0] : (w == 1 ? mask[1] : mask[2]);
@@ -587,7 +599,6 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
         if (w == 0) mask[0] |= bit;
         else if (w == 1) mask[1] |= bit;
         else mask[2] |= bit;
-        sv[t] = v;
       }
     }
     auto is_surv = [&](uint32_t v) {
@@ -618,7 +629,10 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
     for (int t = 0; t < KMAX; ++t) lw[t] = mod255(lw[t]);
 
     for (uint32_t r = 0; r < e; ++r) {
-      const uint32_t l = lidx[r];
+      uint32_t l = 0;
+#pragma unroll
+      for (int q = 0; q < MEMO_EC_MAX_M; ++q)
+        if ((uint32_t)q == r) l = lv[q];
       bad |= l >= nt;
       const bool unit = !bad && is_surv(l);
       uint32_t llam = 0;  // log Lam_l
@@ -626,7 +640,7 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
         uint32_t acc = s_lw0[l];
         for (uint32_t c = 0; c < m; ++c) {
           const uint32_t ci = s_comp[c][tid];
-          if (ci != l) acc += lg[l ^ ci];
+          acc += lg[l ^ ci];  // ci == l adds log[0] = 0
         }
         llam = 255u - mod255(acc);
       }
@@ -681,16 +695,26 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
-  stage_gf(s_gf);
-  __syncthreads();
   const uint32_t k = a.k, e = a.e, nt = a.k + a.m, ek = a.e * a.k;
-  stage_lw0(lg, k, nt, s_lw0);
-  __syncthreads();
   const uint32_t t = threadIdx.x % L;
   const uint64_t b = (uint64_t)blockIdx.x * (256 / L) + threadIdx.x / L;
-  if (b >= a.n) return;  // whole groups; no barrier below
+  const bool live = b < a.n;  // whole groups
   const bool col = t < k;
-  const uint32_t sv = col ? a.surv_idx[b * k + t] : 0u;
+  // The block's indices are loaded first, so their latency overlaps the
+  // table staging: survivor t in lane t, lost shard r in lane r % L.
+  constexpr int NS = (MEMO_EC_MAX_M + L - 1) / L;
+  const uint32_t sv = (live && col) ? a.surv_idx[b * k + t] : 0u;
+  uint32_t lv[NS];
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    const uint32_t r = t + q * L;
+    lv[q] = (live && r < e) ? a.lost_idx[b * e + r] : 0u;
+  }
+  stage_gf(s_gf);
+  __syncthreads();
+  stage_lw0(lg, k, nt, s_lw0);
+  __syncthreads();
+  if (!live) return;  // no barrier below
   bool bad = col && sv >= nt;
   uint32_t mk[3] = {0u, 0u, 0u};
   if (col && sv < nt) {
@@ -716,20 +740,30 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
   uint32_t lw = 0;  // log W_t
   if (col && !bad) {
     lw = s_lw0[sv];
-    for (uint32_t i = 0; i < nt; ++i)
-      if (!is_surv(i)) lw += lg[sv ^ i];
+#pragma unroll 8
+    for (uint32_t i = 0; i < nt; ++i) {
+      const uint32_t v = lg[sv ^ i];
+      lw += is_surv(i) ? 0u : v;
+    }
     lw = mod255(lw);
   }
   uint8_t* out = a.rows + b * (uint64_t)ek;
   for (uint32_t r = 0; r < e; ++r) {
-    const uint32_t l = a.lost_idx[b * e + r];  // the same for the whole group
+    uint32_t mine = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+      if ((uint32_t)q == r / L) mine = lv[q];
+    const uint32_t l = __shfl(mine, r % L, L);  // the same for the whole group
     bad |= l >= nt;
     const bool unit = !bad && is_surv(l);
     uint32_t llam = 0;  // log Lam_l
     if (!bad && !unit) {
-      uint32_t acc = s_lw0[l];
-      for (uint32_t i = 0; i < nt; ++i)
-        if (!is_surv(i) && i != l) acc += lg[l ^ i];
+      uint32_t acc = s_lw0[l];  // i == l adds log[0] = 0
+#pragma unroll 8
+      for (uint32_t i = 0; i < nt; ++i) {
+        const uint32_t v = lg[l ^ i];
+        acc += is_surv(i) ? 0u : v;
+      }
       llam = 255u - mod255(acc);
     }
     if (col) {
