@@ -218,6 +218,47 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
             "bit_exact_vs_gpu": ok_simd and ok_scalar}
 
 
+def c1_case(torch, ec, codec, stream):
+    """BASELINE.json configs[0] (C1): RS(3,2) encode + rebuild (e = 1 and 2
+    random erasures per block) of 1000 x 64 KiB blocks.  The CPU oracle
+    (scalar, all host threads; the reference-runnable case) is timed beside
+    the GPU on the same bytes, and every rebuilt shard is compared across
+    the two (whole batch, bit-exact)."""
+    from oracle import oracle as O
+    k, m, B, n = 3, 2, 65536, 1000
+    S = ec.shard_size(B, k)
+    try:
+        threads = max(1, min(len(os.sched_getaffinity(0)), 16))
+    except AttributeError:
+        threads = 1
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    t0 = time.perf_counter()
+    par = O.encode(k, m, S, data, threads=threads)
+    cpu_enc = time.perf_counter() - t0
+    d = torch.from_numpy(data).cuda()
+    p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+    _, ek = timed_launches(torch, lambda: codec.encode(k, m, d, p), 20, 20, None, stream)
+    ok = bool(np.array_equal(p.cpu().numpy(), par))
+    out = {"workload": "RS(3,2) encode + rebuild (e=1, e=2), 1000 x 65536-byte blocks (BASELINE.json C1)",
+           "cpu_threads": threads, "cpu_kind": "port (scalar table oracle)",
+           "encode": {"cpu_ms": round(cpu_enc * 1e3, 3), "gpu_ms": round(float(np.median(ek)), 4)}}
+    for e in (1, 2):
+        s_idx, l_idx = O.erasures(SEED, 0, n, k, m, e)
+        surv = O.gather(k, m, S, data, par, s_idx)
+        t0 = time.perf_counter()
+        want = O.rebuild(k, m, S, s_idx, surv, l_idx, threads=threads)
+        cpu_reb = time.perf_counter() - t0
+        sd, ld, sv = (torch.from_numpy(x).cuda() for x in (s_idx, l_idx, surv))
+        o = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        _, rk = timed_launches(torch, lambda: codec.rebuild(k, m, sd, sv, ld, o), 20, 20, None, stream)
+        codec.synchronize()
+        ok = ok and bool(np.array_equal(o.cpu().numpy(), want))
+        out["rebuild_e%d" % e] = {"cpu_ms": round(cpu_reb * 1e3, 3),
+                                  "gpu_ms": round(float(np.median(rk)), 4)}
+    out["bit_exact"] = ok
+    return out
+
+
 def main():
     args = parse()
     import torch
@@ -387,6 +428,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         sample = par[:4].cpu().numpy()
         result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, sample)
+        result["c1"] = c1_case(torch, ec, codec, stream)
 
     if args.sha and world == 1:
         import hashlib

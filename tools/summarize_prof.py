@@ -39,8 +39,9 @@ def main():
     mac = st["gf_mac_kernel"]
     trace = [r for r in rows(os.path.join(prof, "trace", "trace_kernel_trace.csv"))
              if r["Kernel_Name"].startswith("gf_mac_kernel")]
-    # bench order: all encode launches, then the rebuilds (one decode-rows
-    # launch each)
+    # bench order: the encode section (warmup + timed launches) comes first;
+    # the rebuild sections follow
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace]
     fetch = [float(r["Counter_Value"]) for r in rows(os.path.join(prof, "fetch", "fetch_counter_collection.csv"))
              if r["Kernel_Name"].startswith("gf_mac_kernel")]
@@ -52,12 +53,11 @@ def main():
         f.write("launch,FETCH_SIZE_KB,WRITE_SIZE_KB\n")
         for i, (a, b) in enumerate(zip(fetch, write)):
             f.write("%d,%.1f,%.1f\n" % (i, a, b))
-    n_reb = sum(int(r["Calls"]) for name, r in st.items() if name.startswith("decode_rows"))
-    enc = durs[:len(durs) - n_reb] if len(durs) > n_reb else durs
     live = None
     for line in open(os.path.join(prof, "trace.log")):
         if line.startswith("{"):
             live = json.loads(line)
+    enc = durs[:live["warmup"] + live["steps"]] if live else durs
     e_avg = statistics.mean(enc)
     tj = os.path.join(out_dir, "pmc_traffic.json")
     t = json.load(open(tj)) if os.path.exists(tj) else {}
