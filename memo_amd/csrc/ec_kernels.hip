@@ -39,7 +39,7 @@ namespace memo_ec {
 // ----------------------------------------------------------------- GF tables
 struct GfTables {
   uint8_t log[256];
-  uint8_t exp[512];
+  uint8_t exp[768];  // exp[i] = 2^(i mod 255): sums of three logs index it unreduced
 };
 
 constexpr GfTables make_gf() {
@@ -51,12 +51,13 @@ constexpr GfTables make_gf() {
     x <<= 1;
     if (x & 0x100) x ^= 0x11D;
   }
-  for (int i = 255; i < 512; ++i) t.exp[i] = t.exp[i - 255];
+  for (int i = 255; i < 768; ++i) t.exp[i] = t.exp[i - 255];
   t.log[0] = 0;
   return t;
 }
 
 __constant__ GfTables kGf = make_gf();
+constexpr int kGfDwords = sizeof(GfTables) / 4;
 const GfTables kGfHost = make_gf();
 
 __host__ __device__ __forceinline__ uint32_t gf_mul_t(const uint8_t* lg, const uint8_t* ex,
@@ -68,10 +69,10 @@ __host__ __device__ __forceinline__ uint32_t gf_inv_t(const uint8_t* lg, const u
   return a ? ex[255 - lg[a]] : 0u;
 }
 
-// Copy the 768-byte log/antilog image into LDS (192 dwords).
+// Copy the 1024-byte log/antilog image into LDS (256 dwords).
 __device__ __forceinline__ void stage_gf(uint32_t* s_gf) {
   const uint32_t* src = reinterpret_cast<const uint32_t*>(&kGf);
-  for (int i = threadIdx.x; i < 192; i += blockDim.x) s_gf[i] = src[i];
+  for (int i = threadIdx.x; i < kGfDwords; i += blockDim.x) s_gf[i] = src[i];
 }
 
 // Product-table dword q of coefficient c.  Image per coefficient: 8 dwords
@@ -543,7 +544,7 @@ __device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_
 
 template <int KMAX>
 __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_gf[192];
+  __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   __shared__ uint8_t s_comp[MEMO_EC_MAX_M][256];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch (staged rows)
@@ -650,7 +651,7 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
           uint32_t v;
           if (bad) v = 0;
           else if (unit) v = sv[t] == l ? 1u : 0u;
-          else v = ex[mod255(lw[t] + llam + 255u - lg[l ^ sv[t]])];
+          else v = ex[lw[t] + llam + 255u - lg[l ^ sv[t]]]  /* < 765 */;
           out[r * k + t] = (uint8_t)v;
         }
       }
@@ -691,7 +692,7 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
 // C3-sized batch instead of ~15.
 template <int L>
 __global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t s_gf[192];
+  __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
@@ -770,7 +771,7 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
       uint32_t v;
       if (bad) v = 0;
       else if (unit) v = sv == l ? 1u : 0u;
-      else v = ex[mod255(lw + llam + 255u - lg[l ^ sv])];
+      else v = ex[lw + llam + 255u - lg[l ^ sv]]  /* < 765 */;
       out[r * k + t] = (uint8_t)v;
     }
   }
