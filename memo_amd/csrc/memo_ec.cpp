@@ -29,9 +29,12 @@ struct memo_ec_ctx {
   // batch slots, and per-slot events chaining the three stages
   hipStream_t sh = nullptr, sk = nullptr, sd = nullptr;
   hipEvent_t ev_h[3] = {}, ev_k[3] = {}, ev_d[3] = {};
+  // orders work after what is pending on `stream` (stream switches; host
+  // rebuilds, whose decode rows share d_tabs with device rebuilds)
+  hipEvent_t ev_order = nullptr;
   uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
   uint32_t* h_status = nullptr;   // pinned copy of d_status for host-memory calls
-  uint32_t* d_tabs = nullptr;     // per-block product-table images (rebuild)
+  uint32_t* d_tabs = nullptr;     // rebuild scratch: per-block decode rows
   size_t tabs_cap = 0;            // bytes
   struct TabEntry {
     int k, m, R, kpad;
@@ -217,6 +220,7 @@ int ensure_tabs(memo_ec_ctx* ctx, size_t bytes) {
     if (int rc = sync_pipeline(ctx)) return rc;
     HIPCHK(hipFree(ctx->d_tabs));
     ctx->d_tabs = nullptr;
+    ctx->tabs_cap = 0;
   }
   const size_t cap = std::max<size_t>(bytes, 1 << 20);
   HIPCHK(hipMalloc(&ctx->d_tabs, cap));
@@ -254,8 +258,11 @@ int sync_pipeline(memo_ec_ctx* ctx) {
 }
 
 int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
+  // capacities drop to 0 before reallocating, so a failed allocation is
+  // retried by the next call instead of leaving null slots behind a cap
   if (dev_bytes > ctx->slot_cap) {
     if (int rc = sync_pipeline(ctx)) return rc;
+    ctx->slot_cap = 0;
     for (auto& p : ctx->d_slot) {
       if (p) HIPCHK(hipFree(p));
       p = nullptr;
@@ -265,6 +272,7 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
   }
   if (host_bytes > ctx->hslot_cap) {
     if (int rc = sync_pipeline(ctx)) return rc;
+    ctx->hslot_cap = 0;
     for (auto& p : ctx->h_slot) {
       if (p) HIPCHK(hipHostFree(p));
       p = nullptr;
@@ -452,6 +460,10 @@ int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
     memo_ec_ctx_destroy(c);
     return rc;
   }
+  if ((rc = hip_rc(hipEventCreateWithFlags(&c->ev_order, hipEventDisableTiming)))) {
+    memo_ec_ctx_destroy(c);
+    return rc;
+  }
   for (int i = 0; i < kSlots; ++i) {
     if ((rc = hip_rc(hipEventCreateWithFlags(&c->ev_h[i], hipEventDisableTiming))) ||
         (rc = hip_rc(hipEventCreateWithFlags(&c->ev_k[i], hipEventDisableTiming))) ||
@@ -487,6 +499,7 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
   for (int i = 0; i < kSlots; ++i)
     for (auto ev : {c->ev_h[i], c->ev_k[i], c->ev_d[i]})
       if (ev) (void)hipEventDestroy(ev);
+  if (c->ev_order) (void)hipEventDestroy(c->ev_order);
   for (auto st : {c->sh, c->sk, c->sd})
     if (st) (void)hipStreamDestroy(st);
   if (c->own) (void)hipStreamDestroy(c->own);
@@ -496,7 +509,15 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
 
 int memo_ec_set_stream(memo_ec_ctx* c, void* s) {
   if (!c) return MEMO_EC_EINVAL;
-  c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+  hipStream_t ns = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+  if (ns != c->stream) {
+    // work on the new stream starts after the old stream's: both reuse the
+    // ctx's scratch (decode rows)
+    DeviceGuard g(c->device);
+    HIPCHK(hipEventRecord(c->ev_order, c->stream));
+    HIPCHK(hipStreamWaitEvent(ns, c->ev_order, 0));
+  }
+  c->stream = ns;
   return MEMO_EC_OK;
 }
 
@@ -585,6 +606,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (int rc = ensure_slots(c, slot, slot)) return rc;
   const size_t tabs = tab_bytes(k, e, nb);
   if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
+  // device rebuilds still pending on the ctx stream read the same scratch
+  HIPCHK(hipEventRecord(c->ev_order, c->stream));
+  HIPCHK(hipStreamWaitEvent(c->sk, c->ev_order, 0));
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
   const int rc = run_pipeline(
       c, n, nb,

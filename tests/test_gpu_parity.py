@@ -374,6 +374,49 @@ def ec_erasures(n, k, m, e):
     return ec.erasures(SEED, 0, n, k, m, e)
 
 
+def test_scratch_reuse_is_ordered(O):
+    """Back-to-back rebuilds that reuse the ctx's decode-row scratch from
+    different queues: an async device rebuild, then a host-memory rebuild
+    (pipeline streams), then a switch to another stream and a second device
+    rebuild.  Each must read its own rows."""
+    import torch
+    from memo_amd import ec
+    k, m, B, n = 10, 4, 1 << 20, 64
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 77, n, B, k, S)
+    par = O.encode(k, m, S, data, threads=4)
+    cases = []
+    for e, seed in ((4, 1), (2, 2), (3, 3)):
+        s, l = O.erasures(SEED + seed, 77, n, k, m, e)
+        cases.append((s, l, O.gather(k, m, S, data, par, s), O.gather(k, m, S, data, par, l)))
+    with ec.Codec(0) as c:
+        st_a, st_b = torch.cuda.Stream(), torch.cuda.Stream()
+        c.set_stream(st_a)
+        s, l, sv, want0 = cases[0]
+        with torch.cuda.stream(st_a):
+            sd, ld, svd = dev(s), dev(l), dev(sv)
+            out0 = empty(n, 4 * S)
+        torch.cuda.synchronize()
+        c.rebuild(k, m, sd, svd, ld, out0)                   # async on st_a
+        s1, l1, sv1, want1 = cases[1]
+        out1 = np.zeros((n, 2 * S), np.uint8)
+        c.rebuild(k, m, s1, sv1, l1, out1)                   # host pipeline
+        s2, l2, sv2, want2 = cases[2]
+        with torch.cuda.stream(st_b):
+            sd2, ld2, svd2 = dev(s2), dev(l2), dev(sv2)
+            out2 = empty(n, 3 * S)
+        torch.cuda.synchronize()
+        c.set_stream(st_a)
+        c.rebuild(k, m, sd, svd, ld, out0)
+        c.set_stream(st_b)
+        c.rebuild(k, m, sd2, svd2, ld2, out2)                # async on st_b
+        c.synchronize()
+        torch.cuda.synchronize()
+        assert np.array_equal(out1, want1)
+        assert np.array_equal(host(out0), want0)
+        assert np.array_equal(host(out2), want2)
+
+
 def test_hip_graph_capture_replay(codec, O):
     """Device-resident encode + rebuild captured into one HIP graph (via
     torch.cuda.CUDAGraph on ROCm) and replayed on new inputs: launch-bound
