@@ -82,7 +82,7 @@ struct DecodeArgs {
   const uint8_t* surv_idx;
   const uint8_t* lost_idx;
   uint8_t* rows;          // n x e x k decode rows
-  uint32_t* status;
+  uint32_t* status;       // set to 1 on an invalid survivor set (device or pinned host word)
   uint64_t n;
   uint32_t k, m, e;
   uint32_t pitch;         // decode_coef_kernel: LDS row-staging pitch (set by the launcher)

@@ -283,6 +283,17 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
   return MEMO_EC_OK;
 }
 
+// Host-memory calls moving at most this many bytes (in + out) run their
+// kernels on pinned host memory directly, with no DMA copies: 5-40% less
+// time than the copy pipeline up to ~8 MiB of input, more beyond, where the
+// pipeline's copy overlap and threaded bounce copies win
+// (profiles/r01_zero_copy_probe.jsonl).  MEMO_EC_ZC_KB overrides (read per
+// call; 0 disables).
+size_t zc_max_bytes() {
+  const char* p = std::getenv("MEMO_EC_ZC_KB");
+  return p ? (size_t)std::strtoull(p, nullptr, 10) << 10 : (size_t)4 << 20;
+}
+
 // Largest batch (blocks) one MAC launch takes: tiles must fit a 31-bit grid.
 // MEMO_EC_MAX_LAUNCH_TILES lowers the bound so tests can reach the split
 // path without a 2^31-tile batch.
@@ -319,13 +330,13 @@ int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint
 // its rows.  `scratch` has room for tab_bytes(k, e, n).
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
-                   void* scratch, hipStream_t st) {
+                   void* scratch, hipStream_t st, uint32_t* status = nullptr) {
   const int KC = mac_kchunk(k), R = mac_rbound(e);
   const size_t step = max_blocks_per_launch(S);
   uint8_t* rows = static_cast<uint8_t*>(scratch);
   const uint64_t row_b = (uint64_t)e * k;
-  DecodeArgs a{surv_idx, lost_idx, rows, ctx->d_status, n, (uint32_t)k, (uint32_t)m,
-               (uint32_t)e, 0};
+  DecodeArgs a{surv_idx, lost_idx, rows, status ? status : ctx->d_status, n, (uint32_t)k,
+               (uint32_t)m, (uint32_t)e, 0};
   HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
@@ -541,9 +552,25 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
   const size_t in_b = (size_t)k * S, out_b = (size_t)m * S;
+  const bool pinned = where == MEMO_EC_HOST_PINNED;
+  if (n * (in_b + out_b) <= zc_max_bytes()) {
+    // Small call: the kernel reads the blocks from, and writes the parity
+    // to, pinned host memory over PCIe -- no DMA copies to wait for.
+    if (int rc = ensure_slots(c, 0, pinned ? 0 : n * (in_b + out_b))) return rc;
+    const uint8_t* src = data;
+    uint8_t* dst = parity;
+    if (!pinned) {
+      std::memcpy(c->h_slot[0], data, n * in_b);
+      src = c->h_slot[0];
+      dst = c->h_slot[0] + n * in_b;
+    }
+    if (int rc = encode_device(c, k, m, S, n, src, dst, c->sk)) return rc;
+    HIPCHK(hipStreamSynchronize(c->sk));
+    if (!pinned) std::memcpy(parity, dst, n * out_b);
+    return MEMO_EC_OK;
+  }
   size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
   nb = std::min(nb, n);
-  const bool pinned = where == MEMO_EC_HOST_PINNED;
   if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
   // slot layout (device and pageable bounce): [data nb*in_b | parity nb*out_b]
   return run_pipeline(
@@ -592,23 +619,61 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   DeviceGuard g(c->device);
   if (where == MEMO_EC_DEVICE) {
     if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
-    return rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_tabs, c->stream);
+    if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_tabs,
+                                c->stream))
+      return rc;
+    // marks the scratch busy until this rebuild is done (host calls check it)
+    return hip_rc(hipEventRecord(c->ev_order, c->stream));
   }
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
   const size_t in_b = (size_t)k * S, out_b = (size_t)e * S;
   const size_t idx_b = (size_t)k + e;
+  const bool pinned = where == MEMO_EC_HOST_PINNED;
+  // device rebuilds still pending on the ctx stream read the same scratch
+  const hipError_t q = hipEventQuery(c->ev_order);
+  if (q == hipErrorNotReady) {
+    HIPCHK(hipStreamWaitEvent(c->sk, c->ev_order, 0));
+  } else if (q != hipSuccess) {
+    return hip_rc(q);
+  }
+  if (n * (in_b + out_b + idx_b) + 4 <= zc_max_bytes()) {
+    // Small call: decode and MAC run on pinned host memory directly (the
+    // survivors, indices and output in the bounce slot, or the caller's
+    // pinned buffers); the status word rides in the slot too.
+    const size_t slot = n * (in_b + out_b + idx_b) + 64;
+    if (int rc = ensure_slots(c, 0, slot)) return rc;
+    if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
+    uint8_t* h = c->h_slot[0];
+    uint8_t* h_sidx = h + n * (in_b + out_b);
+    uint8_t* h_lidx = h_sidx + n * k;
+    uint32_t* h_st = reinterpret_cast<uint32_t*>(h + ((n * (in_b + out_b + idx_b) + 3) & ~(size_t)3));
+    std::memcpy(h_sidx, surv_idx, n * k);
+    std::memcpy(h_lidx, lost_idx, n * e);
+    *h_st = 0;
+    const uint8_t* sv = surv;
+    uint8_t* ov = out;
+    if (!pinned) {
+      std::memcpy(h, surv, n * in_b);
+      sv = h;
+      ov = h + n * in_b;
+    }
+    if (int rc = rebuild_device(c, k, m, S, n, h_sidx, sv, h_lidx, e, ov, c->d_tabs, c->sk, h_st))
+      return rc;
+    HIPCHK(hipStreamSynchronize(c->sk));
+    if (!pinned) std::memcpy(out, ov, n * out_b);
+    int drc = c->deferred;
+    c->deferred = 0;
+    if (drc == MEMO_EC_OK && (__atomic_load_n(h_st, __ATOMIC_ACQUIRE) & 1u)) drc = MEMO_EC_ESINGULAR;
+    return drc;
+  }
   size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
   nb = std::min(nb, n);
-  const bool pinned = where == MEMO_EC_HOST_PINNED;
   // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e]
   const size_t slot = nb * (in_b + out_b + idx_b);
   if (int rc = ensure_slots(c, slot, slot)) return rc;
   const size_t tabs = tab_bytes(k, e, nb);
   if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
-  // device rebuilds still pending on the ctx stream read the same scratch
-  HIPCHK(hipEventRecord(c->ev_order, c->stream));
-  HIPCHK(hipStreamWaitEvent(c->sk, c->ev_order, 0));
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
   const int rc = run_pipeline(
       c, n, nb,

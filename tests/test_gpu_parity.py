@@ -255,6 +255,33 @@ def test_host_memory_paths(codec, O):
     assert np.array_equal(out, O.gather(k, m, S, data, want, l))
 
 
+@pytest.mark.parametrize("zc_kb", ["256", "0"])
+def test_small_host_calls(codec, O, zc_kb, monkeypatch):
+    """One-block and few-block calls from pageable and pinned host memory,
+    with the zero-copy path (kernels on pinned host memory, MEMO_EC_ZC_KB
+    default) and without it (DMA copies)."""
+    import torch
+    monkeypatch.setenv("MEMO_EC_ZC_KB", zc_kb)
+    k, m = 10, 4
+    for B, n in ((4096, 1), (100000, 3), (4096, 7)):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 500 + n, n, B, k, S)
+        want = O.encode(k, m, S, data)
+        par = np.zeros((n, m * S), np.uint8)
+        codec.encode(k, m, data, par)
+        assert np.array_equal(par, want), (B, n)
+        pd = torch.from_numpy(data).pin_memory()
+        pp = torch.zeros((n, m * S), dtype=torch.uint8).pin_memory()
+        codec.encode(k, m, pd, pp)
+        assert np.array_equal(pp.numpy(), want), (B, n)
+        for e in (1, m):
+            s, l = O.erasures(SEED, 500 + n, n, k, m, e)
+            surv = O.gather(k, m, S, data, want, s)
+            out = np.zeros((n, e * S), np.uint8)
+            codec.rebuild(k, m, s, surv, l, out)
+            assert np.array_equal(out, O.gather(k, m, S, data, want, l)), (B, n, e)
+
+
 def test_singular_survivors_reported(codec):
     from memo_amd import ec
     k, m, S, n = 4, 2, 64, 2
@@ -292,13 +319,15 @@ def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
     codec.synchronize()
 
 
-def test_singular_survivors_reported_host_paths(codec, O, monkeypatch):
+@pytest.mark.parametrize("B,n", [(1 << 16, 40), (4096, 5)])
+def test_singular_survivors_reported_host_paths(codec, O, monkeypatch, B, n):
     """Host-memory rebuilds report a bad survivor set from any pipeline batch
-    (the status word is read behind the last batch), the good blocks are
+    (the status word is read behind the last batch) or from a small
+    zero-copy call (status word in the pinned slot), the good blocks are
     still rebuilt, and the error does not leak into the next call."""
     import torch
     from memo_amd import ec
-    k, m, B, n = 4, 2, 1 << 16, 40
+    k, m = 4, 2
     S = O.shard_size(B, k)
     monkeypatch.setenv("MEMO_EC_PIPE_MB", "1")  # several pipeline batches
     c2 = ec.Codec(0)  # the pipeline size is read at ctx creation
