@@ -330,6 +330,8 @@ def test_singular_survivors_reported_host_paths(codec, O, monkeypatch, B, n):
     k, m = 4, 2
     S = O.shard_size(B, k)
     monkeypatch.setenv("MEMO_EC_PIPE_MB", "1")  # several pipeline batches
+    if n > 5:
+        monkeypatch.setenv("MEMO_EC_ZC_KB", "0")  # the copy pipeline, not zero-copy
     c2 = ec.Codec(0)  # the pipeline size is read at ctx creation
     data = O.fill_blocks(SEED, 0, n, B, k, S)
     par = O.encode(k, m, S, data)
