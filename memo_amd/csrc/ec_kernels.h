@@ -32,6 +32,10 @@
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
 #endif
+// 1: straight-line bodies for k = 6, 12, 14 (R <= 4) besides 2, 3, 4, 10, 16
+#ifndef MEMO_EC_MAC_EXTRA_KC
+#define MEMO_EC_MAC_EXTRA_KC 1
+#endif
 
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
@@ -111,9 +115,9 @@ struct GatherArgs {
 };
 
 // Compile-time output bound R >= r (rows r..R-1 are zero) and shard chunk KC
-// (shards beyond kin inside the last chunk are zero) used for (kin, r).
+// (shards beyond kin inside the last chunk are zero) used for (kin, R).
 int mac_rbound(int r);
-int mac_kchunk(int kin);
+int mac_kchunk(int kin, int R);
 void table_image_host(const uint8_t* coef, uint32_t r, uint32_t kin, uint32_t R, uint32_t kpad,
                       uint32_t* out);
 hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,

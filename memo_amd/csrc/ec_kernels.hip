@@ -1002,10 +1002,27 @@ int mac_rbound(int r) {
   return 16;
 }
 
-int mac_kchunk(int kin) {
+int mac_kchunk(int kin, int R) {
   switch (kin) {
     case 2: case 3: case 4: case 10: case 16: return kin;
+#if MEMO_EC_MAC_EXTRA_KC
+    case 6: case 12: case 14: return R <= 4 ? kin : 4;  // instantiated for R <= 4 only
+#endif
     default: return 4;
+  }
+}
+
+// Shard chunks instantiated only for R <= 4 (common codes: RS(6,3),
+// RS(12,4), RS(14,4)); larger R takes the 4-shard chunk loop.
+template <int KC>
+static hipError_t launch_mac_r4(int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+                                hipStream_t st) {
+  switch (R) {
+    case 1: return launch_mac_t<KC, 1>(coef, L, grid, lds, st);
+    case 2: return launch_mac_t<KC, 2>(coef, L, grid, lds, st);
+    case 3: return launch_mac_t<KC, 3>(coef, L, grid, lds, st);
+    case 4: return launch_mac_t<KC, 4>(coef, L, grid, lds, st);
+    default: return hipErrorInvalidValue;
   }
 }
 
@@ -1016,6 +1033,11 @@ hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t gri
     case 3: return launch_mac_r<3>(R, coef, L, grid, lds, st);
     case 4: return launch_mac_r<4>(R, coef, L, grid, lds, st);
     case 10: return launch_mac_r<10>(R, coef, L, grid, lds, st);
+#if MEMO_EC_MAC_EXTRA_KC
+    case 6: return launch_mac_r4<6>(R, coef, L, grid, lds, st);
+    case 12: return launch_mac_r4<12>(R, coef, L, grid, lds, st);
+    case 14: return launch_mac_r4<14>(R, coef, L, grid, lds, st);
+#endif
     case 16: return launch_mac_r<16>(R, coef, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }

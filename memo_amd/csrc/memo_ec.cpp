@@ -310,7 +310,7 @@ size_t max_blocks_per_launch(size_t S) {
 // Device-resident encode on stream st.
 int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* data,
                   uint8_t* parity, hipStream_t st) {
-  const int KC = mac_kchunk(k), R = mac_rbound(m);
+  const int R = mac_rbound(m), KC = mac_kchunk(k, R);
   const uint32_t* tab = nullptr;
   if (int rc = encode_tables(ctx, k, m, R, KC, &tab)) return rc;
   const size_t step = max_blocks_per_launch(S);
@@ -331,7 +331,7 @@ int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
                    void* scratch, hipStream_t st, uint32_t* status = nullptr) {
-  const int KC = mac_kchunk(k), R = mac_rbound(e);
+  const int R = mac_rbound(e), KC = mac_kchunk(k, R);
   const size_t step = max_blocks_per_launch(S);
   uint8_t* rows = static_cast<uint8_t*>(scratch);
   const uint64_t row_b = (uint64_t)e * k;
@@ -722,7 +722,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
 
 int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* segs) {
   if (!c || nseg < 0 || nseg > MEMO_EC_MAX_SEGMENTS || (nseg && !segs)) return MEMO_EC_EINVAL;
-  // Segments are grouped by shard-chunk class (mac_kchunk(k)): each class is
+  // Segments are grouped by shard-chunk class (mac_kchunk): each class is
   // one launch of its own straight-line body, with R = the class's largest
   // m bound (smaller m's rows are zero tables); the launches go back to back
   // on the ctx stream.  One launch across classes would force every segment
@@ -737,7 +737,7 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
     if (segs[i].S == 0 || segs[i].S % 64 || !segs[i].data || !segs[i].parity)
       return MEMO_EC_EINVAL;
     if (segs[i].n > max_blocks_per_launch(segs[i].S)) return MEMO_EC_ERANGE;
-    const int kc = mac_kchunk(segs[i].k);
+    const int kc = mac_kchunk(segs[i].k, mac_rbound(segs[i].m));
     size_t ci = 0;
     while (ci < classes.size() && classes[ci] != kc) ++ci;
     if (ci == classes.size()) {
@@ -753,7 +753,7 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
     const int KC = classes[ci], R = cls_R[ci];
     for (int i = 0; i < nseg; ++i) {
       const auto& s = segs[i];
-      if (s.m == 0 || s.n == 0 || mac_kchunk(s.k) != KC) continue;
+      if (s.m == 0 || s.n == 0 || mac_kchunk(s.k, mac_rbound(s.m)) != KC) continue;
       const uint32_t* tab = nullptr;
       if (int rc = encode_tables(c, s.k, s.m, R, KC, &tab)) return rc;
       launches[ci].push_back(plan_segment((uint32_t)s.k, (uint32_t)s.m, s.S, s.n, s.data,

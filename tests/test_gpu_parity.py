@@ -63,8 +63,8 @@ def test_golden_cases(codec, golden, O):
         assert np.array_equal(host(out), host(want)), ci
 
 
-CONFIGS = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (6, 6), (8, 5), (10, 4), (12, 7), (16, 4),
-           (20, 8), (33, 12), (64, 16)]
+CONFIGS = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (6, 3), (6, 6), (8, 5), (10, 4), (12, 4),
+           (12, 7), (14, 2), (16, 4), (20, 8), (33, 12), (64, 16)]
 
 
 @pytest.mark.parametrize("k,m", CONFIGS)
@@ -218,6 +218,7 @@ def test_mixed_segments_one_launch(codec, O):
 @pytest.mark.parametrize("codes", [
     [(3, 2, 5000, 9), (7, 3, 70000, 4), (20, 4, 300000, 3), (12, 1, 4096, 40), (16, 4, 4096, 33)],
     [(4, 2, 4096, 5), (10, 6, 100000, 2), (2, 1, 64, 300)],  # R > 4: the chunk loop
+    [(6, 3, 4096, 9), (6, 6, 30000, 3), (12, 4, 70000, 2), (14, 1, 4096, 20), (12, 5, 999, 7)],
 ])
 def test_mixed_segments_any_k(codec, O, codes):
     """Mixed k in one launch, including k outside {4, 10, 16}, k > 16 and
