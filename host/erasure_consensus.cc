@@ -305,7 +305,7 @@ void ErasureConsensus::batcher_loop() {
 }
 
 // Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360).
-void ErasureConsensus::place(const Block& b, const Buffer& parity) {
+void ErasureConsensus::place(const Block& b, const Buffer& parity, bool parallel) {
   const int total = o_.k + o_.m;
   const size_t S = memo_ec_shard_size(b.data.size(), o_.k);
   const Buffer data = padded(b, S);
@@ -318,7 +318,7 @@ void ErasureConsensus::place(const Block& b, const Buffer& parity) {
   pl.salt = b.salt;
   pl.owner.assign(total, Address());
   std::vector<int> ok(total, 0);
-  pool_.parallel_for(owners.size(), [&](size_t i) {
+  auto put = [&](size_t i) {
     ShardHeader h;
     h.k = (uint8_t)o_.k;
     h.m = (uint8_t)o_.m;
@@ -333,7 +333,10 @@ void ErasureConsensus::place(const Block& b, const Buffer& parity) {
       ok[i] = 1;
     } catch (Unavailable&) {
     }
-  });
+  };
+  if (parallel) pool_.parallel_for(owners.size(), put);
+  else
+    for (size_t i = 0; i < owners.size(); ++i) put(i);
   int reached = 0;
   for (size_t i = 0; i < owners.size(); ++i)
     if (ok[i]) {
@@ -369,12 +372,20 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
     if (b.is_mutable || b.address.mutable_block()) backend_->store(b, STORE_INSERT);
     else imm.push_back(&b);
   }
+  // The per-block host work (CHB address check, copies into the batch,
+  // shard framing + stores) runs on the pool, one block per task; the
+  // encode is one GPU call per shard-size bucket.
   for (size_t b0 = 0; b0 < imm.size(); b0 += o_.batch_max) {
     const size_t n0 = std::min<size_t>(o_.batch_max, imm.size() - b0);
+    std::vector<char> valid(n0, 0);
+    pool_.parallel_for(n0, [&](size_t i) {
+      const Block* b = imm[b0 + i];
+      valid[i] = chb_valid(b->address, b->salt, b->data);
+    });
     std::map<int, std::vector<const Block*>> by_s;
     for (size_t i = 0; i < n0; ++i) {
       const Block* b = imm[b0 + i];
-      if (!chb_valid(b->address, b->salt, b->data)) throw ValidationFailed("CHB address mismatch");
+      if (!valid[i]) throw ValidationFailed("CHB address mismatch");
       by_s[size_bucket(memo_ec_shard_size(b->data.size(), o_.k))].push_back(b);
     }
     for (auto& g : by_s) {
@@ -382,75 +393,106 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
       size_t S = 0;
       for (auto* b : g.second) S = std::max(S, memo_ec_shard_size(b->data.size(), o_.k));
       Buffer data(n * o_.k * S, 0), parity(n * o_.m * S);
-      for (size_t i = 0; i < n; ++i) {
+      pool_.parallel_for(n, [&](size_t i) {
         const auto& d = g.second[i]->data;
         const size_t Sb = memo_ec_shard_size(d.size(), o_.k);
         for (int j = 0; j < o_.k; ++j) {
           const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
           std::copy(d.begin() + lo, d.begin() + hi, data.begin() + (i * o_.k + j) * S);
         }
-      }
+      });
       codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
-      // place() fans out over the pool itself; do not nest pool work here
-      for (size_t i = 0; i < n; ++i) {
+      pool_.parallel_for(n, [&](size_t i) {
         const size_t Sb = memo_ec_shard_size(g.second[i]->data.size(), o_.k);
         Buffer p((size_t)o_.m * Sb);
         for (int r = 0; r < o_.m; ++r)
           std::copy(parity.begin() + (i * o_.m + r) * S, parity.begin() + (i * o_.m + r) * S + Sb,
                     p.begin() + (size_t)r * Sb);
-        place(*g.second[i], p);
-      }
+        place(*g.second[i], p, /*parallel=*/false);  // already on the pool
+      });
     }
   }
 }
 
-// Shards of block `a` from the nodes in lookup order, in waves, until `want`
-// distinct valid shards are in hand.  Invalid shards count as erasures.
-// parallel = false fetches node by node (for callers already on the pool).
+// Shards of block `a` until `want` distinct valid shards are in hand.
+// Invalid shards count as erasures.  First from the owners the placement
+// index records (Paxos::_node_blocks analogue): shard i from owner i, data
+// shards first.  Then, for blocks this client did not place or shards that
+// moved, from every node in lookup order, in waves.  parallel = false works
+// node by node (for callers already on the pool).
 std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
                                                                     bool& any_down,
                                                                     ShardHeader* hdr,
                                                                     bool parallel) {
   const int total = o_.k + o_.m;
-  auto nodes = overlay_.lookup(a, (int)overlay_.nodes().size());
+  std::vector<Key> keys(total);
+  for (int i = 0; i < total; ++i) keys[i] = shard_key(a, i);
   std::map<int, Buffer> got;
   std::mutex gm;
   any_down = false;
-  size_t next = 0;
-  auto from_node = [&](const std::shared_ptr<Node>& nd) {
-    for (int i = 0; i < total; ++i) {
-      {
-        std::lock_guard<std::mutex> g(gm);
-        if (got.count(i)) continue;
-      }
-      Buffer wire;
-      try {
-        wire = nd->fetch(shard_key(a, i));
-      } catch (Unavailable&) {
-        std::lock_guard<std::mutex> g(gm);
-        any_down = true;
-        return;
-      } catch (silo::MissingKey&) {
-        continue;
-      }
-      try {
-        ShardHeader h = decode_shard(wire, nullptr);
-        if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) continue;
-        std::lock_guard<std::mutex> g(gm);
-        if (hdr && got.empty()) *hdr = h;
-        got.emplace(i, std::move(wire));
-      } catch (ValidationFailed&) {
-        // corrupted shard: an erasure
-      }
-    }
+  auto have = [&](int i) {
+    std::lock_guard<std::mutex> g(gm);
+    return got.count(i) != 0;
   };
-  while ((int)got.size() < want && next < nodes.size()) {
-    const size_t wave = std::min(nodes.size() - next, (size_t)std::max(total, 1));
-    if (parallel)
-      pool_.parallel_for(wave, [&](size_t w) { from_node(nodes[next + w]); });
+  auto count = [&] {
+    std::lock_guard<std::mutex> g(gm);
+    return (int)got.size();
+  };
+  // fetch shard i from nd; true if the node was reachable
+  auto try_node = [&](const std::shared_ptr<Node>& nd, int i) -> bool {
+    Buffer wire;
+    try {
+      if (!nd->try_fetch(keys[i], wire)) return true;
+    } catch (Unavailable&) {
+      std::lock_guard<std::mutex> g(gm);
+      any_down = true;
+      return false;
+    }
+    try {
+      ShardHeader h = decode_shard(wire, nullptr);
+      if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) return true;
+      std::lock_guard<std::mutex> g(gm);
+      if (hdr && got.empty()) *hdr = h;
+      got.emplace(i, std::move(wire));
+    } catch (ValidationFailed&) {
+      // corrupted shard: an erasure
+    }
+    return true;
+  };
+  auto run = [&](size_t n, const std::function<void(size_t)>& fn) {
+    if (parallel && n > 1) pool_.parallel_for(n, fn);
     else
-      for (size_t w = 0; w < wave && (int)got.size() < want; ++w) from_node(nodes[next + w]);
-    next += wave;
+      for (size_t t = 0; t < n && count() < want; ++t) fn(t);
+  };
+
+  std::vector<std::shared_ptr<Node>> owner(total);
+  {
+    std::lock_guard<std::mutex> g(index_mu_);
+    auto it = index_.find(a);
+    if (it != index_.end())
+      for (int i = 0; i < total && i < (int)it->second.owner.size(); ++i)
+        if (it->second.owner[i]) owner[i] = overlay_.node(it->second.owner[i]);
+  }
+  for (int pass = 0; pass < 2 && count() < want; ++pass) {
+    // pass 0: the data shards (no decode needed); pass 1: the parity shards
+    std::vector<int> ids;
+    for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i)
+      if (owner[i] && !owner[i]->evicted && !have(i)) ids.push_back(i);
+    run(ids.size(), [&](size_t t) { try_node(owner[ids[t]], ids[t]); });
+  }
+
+  if (count() < want) {
+    auto nodes = overlay_.lookup(a, (int)overlay_.nodes().size());
+    auto from_node = [&](const std::shared_ptr<Node>& nd) {
+      for (int i = 0; i < total; ++i)
+        if (!have(i) && !try_node(nd, i)) return;  // down: skip the node
+    };
+    size_t next = 0;
+    while (count() < want && next < nodes.size()) {
+      const size_t wave = std::min(nodes.size() - next, (size_t)std::max(total, 1));
+      run(wave, [&](size_t w) { from_node(nodes[next + w]); });
+      next += wave;
+    }
   }
   std::vector<std::pair<int, Buffer>> out;
   for (auto& kv : got) out.emplace_back(kv.first, std::move(kv.second));
@@ -616,30 +658,37 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
     Placement pl;
     std::vector<int> lost, surv;
   };
-  std::vector<Todo> todo;
+  // scan every placed block's shards (on the pool; the index is copied
+  // first so the scan does not hold its lock)
+  std::vector<Todo> all;
   {
     std::lock_guard<std::mutex> g(index_mu_);
-    for (auto& kv : index_) {
-      ++rep.blocks_checked;
-      Todo t{kv.first, kv.second, {}, {}};
-      for (int i = 0; i < total; ++i) {
-        const Address& o = kv.second.owner[i];
-        auto nd = o ? overlay_.node(o) : nullptr;
-        bool ok = nd && !nd->evicted && (nd->up || !include_down);
-        if (ok && nd->up) ok = nd->has(shard_key(kv.first, i));
-        if (ok) {
-          if (nd->up) t.surv.push_back(i);
-        } else {
-          t.lost.push_back(i);
-        }
+    all.reserve(index_.size());
+    for (auto& kv : index_) all.push_back(Todo{kv.first, kv.second, {}, {}});
+  }
+  rep.blocks_checked = all.size();
+  pool_.parallel_for(all.size(), [&](size_t b) {
+    Todo& t = all[b];
+    for (int i = 0; i < total; ++i) {
+      const Address& o = t.pl.owner[i];
+      auto nd = o ? overlay_.node(o) : nullptr;
+      bool ok = nd && !nd->evicted && (nd->up || !include_down);
+      if (ok && nd->up) ok = nd->has(shard_key(t.a, i));
+      if (ok) {
+        if (nd->up) t.surv.push_back(i);
+      } else {
+        t.lost.push_back(i);
       }
-      if (t.lost.empty()) continue;
-      if ((int)t.surv.size() < k) {
-        ++rep.unrecoverable;
-        continue;
-      }
-      todo.push_back(std::move(t));
     }
+  });
+  std::vector<Todo> todo;
+  for (auto& t : all) {
+    if (t.lost.empty()) continue;
+    if ((int)t.surv.size() < k) {
+      ++rep.unrecoverable;
+      continue;
+    }
+    todo.push_back(std::move(t));
   }
   // batches of blocks with the same (S, e): one GPU rebuild call each
   std::map<std::pair<int, size_t>, std::vector<Todo*>> groups;

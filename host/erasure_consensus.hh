@@ -154,7 +154,8 @@ class ErasureConsensus : public StackedConsensus {
   std::unique_ptr<Block> assemble(const Address& a, Gathered& g, const uint8_t* rebuilt,
                                   size_t stride);
   Buffer padded(const Block& b, size_t S) const;
-  void place(const Block& b, const Buffer& parity);
+  // parallel = false stores the shards one by one (callers on the pool).
+  void place(const Block& b, const Buffer& parity, bool parallel = true);
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);

@@ -84,6 +84,33 @@ int Silo::erase(const Key& k) {
   return delta;
 }
 
+bool Silo::_try_get(const Key& k, Buffer& out) const {
+  try {
+    out = _get(k);
+    return true;
+  } catch (silo::MissingKey&) {
+    return false;
+  }
+}
+
+bool Silo::_contains(const Key& k) const {
+  Buffer tmp;
+  return _try_get(k, tmp);
+}
+
+bool MemorySilo::_contains(const Key& k) const {
+  std::lock_guard<std::mutex> g(mu_);
+  return blocks_.count(k) != 0;
+}
+
+bool MemorySilo::_try_get(const Key& k, Buffer& out) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = blocks_.find(k);
+  if (it == blocks_.end()) return false;
+  out = it->second;
+  return true;
+}
+
 Buffer MemorySilo::_get(const Key& k) const {
   std::lock_guard<std::mutex> g(mu_);
   auto it = blocks_.find(k);
@@ -140,14 +167,13 @@ void Node::remove(const Key& k) {
   silo->erase(k);
 }
 
-bool Node::has(const Key& k) const {
-  try {
-    silo->get(k);
-    return true;
-  } catch (silo::MissingKey&) {
-    return false;
-  }
+bool Node::try_fetch(const Key& k, Buffer& out) const {
+  if (!up || evicted) throw Unavailable("node down");
+  const_cast<Node*>(this)->fetches++;
+  return silo->try_get(k, out);
 }
+
+bool Node::has(const Key& k) const { return silo->contains(k); }
 
 std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo> silo) {
   auto n = std::make_shared<Node>();
@@ -170,11 +196,28 @@ std::vector<std::shared_ptr<Node>> Overlay::nodes() const {
   return nodes_;
 }
 
+namespace {
+// Rendezvous score of (address, node): a 64-bit mix of both ids (the ids are
+// already hashes; the ranking needs dispersion, not collision resistance).
+uint64_t rendezvous(const Address& a, const Address& n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int w = 0; w < 4; ++w) {
+    uint64_t x, y;
+    std::memcpy(&x, a.value.data() + 8 * w, 8);
+    std::memcpy(&y, n.value.data() + 8 * w, 8);
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h ^= y * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 31)) * 0x94D049BB133111EBull;
+  }
+  return h ^ (h >> 29);
+}
+}  // namespace
+
 std::vector<std::shared_ptr<Node>> Overlay::rank(const Address& address) const {
   auto all = nodes();
-  std::vector<std::pair<std::array<uint8_t, 32>, std::shared_ptr<Node>>> scored;
-  for (auto& n : all)
-    scored.push_back({sha256(address.value.data(), 32, n->id.value.data(), 32), n});
+  std::vector<std::pair<uint64_t, std::shared_ptr<Node>>> scored;
+  scored.reserve(all.size());
+  for (auto& n : all) scored.push_back({rendezvous(address, n->id), n});
   std::sort(scored.begin(), scored.end(),
             [](const auto& a, const auto& b) { return a.first < b.first; });
   std::vector<std::shared_ptr<Node>> out;

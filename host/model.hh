@@ -121,6 +121,9 @@ class Silo {
   explicit Silo(int64_t capacity = -1) : capacity_(capacity) {}
   virtual ~Silo() = default;
   Buffer get(const Key& k) const { return _get(k); }
+  // get() without the MissingKey exception: false when absent.
+  bool try_get(const Key& k, Buffer& out) const { return _try_get(k, out); }
+  bool contains(const Key& k) const { return _contains(k); }
   // insert: accept a new key; update: accept an existing key.
   int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
   int erase(const Key& k);
@@ -131,6 +134,8 @@ class Silo {
 
  protected:
   virtual Buffer _get(const Key& k) const = 0;
+  virtual bool _try_get(const Key& k, Buffer& out) const;  // default: _get + catch
+  virtual bool _contains(const Key& k) const;                // default: _try_get
   virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
   virtual int _erase(const Key& k) = 0;
   virtual std::vector<Key> _list() = 0;
@@ -146,6 +151,8 @@ class MemorySilo : public Silo {
 
  protected:
   Buffer _get(const Key& k) const override;
+  bool _try_get(const Key& k, Buffer& out) const override;
+  bool _contains(const Key& k) const override;
   int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
   int _erase(const Key& k) override;
   std::vector<Key> _list() override;
@@ -170,6 +177,9 @@ struct Node {
 
   void store(const Key& k, const Buffer& v);
   Buffer fetch(const Key& k) const;
+  // fetch() that reports a missing key by returning false (no exception);
+  // throws Unavailable when the node is down.
+  bool try_fetch(const Key& k, Buffer& out) const;
   void remove(const Key& k);
   bool has(const Key& k) const;
 };

@@ -48,3 +48,19 @@ def test_plugin_semantics_on_gpu():
     r = _run()
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 failed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_plugin_bench_round_trip_on_gpu():
+    """host/tests/bench_plugin.cc end to end at a small size: store, healthy
+    and degraded multi-fetch, repair after eviction, against replication;
+    it exits non-zero if any block comes back wrong or is unrecoverable."""
+    import json
+    _build()
+    r = subprocess.run([os.path.join(HOST, "_build", "bench_plugin"), "96", "70000"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["erasure"]["fetch_ok"] and d["erasure"]["degraded_ok"]
+    assert d["erasure"]["repaired_blocks"] > 0 and d["erasure"]["unrecoverable"] == 0
+    assert d["erasure"]["degraded_codec_calls"] >= 1
