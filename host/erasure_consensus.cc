@@ -174,30 +174,51 @@ void ThreadPool::worker() {
   }
 }
 
+// Items are claimed from a shared counter by up to `threads` pool tasks and
+// by the calling thread itself, so n tiny items cost n atomic increments, not
+// n queue round trips.  The caller returns once every item has run; tasks
+// that start late find no item left and only drop their reference to the
+// shared state.
 void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
   if (n == 0) return;
-  std::mutex dm;
-  std::condition_variable dcv;
-  size_t done = 0;
-  std::exception_ptr err;
+  struct State {
+    std::atomic<size_t> next{0};
+    std::mutex dm;
+    std::condition_variable dcv;
+    size_t done = 0;
+    std::exception_ptr err;
+  };
+  auto st = std::make_shared<State>();
+  const std::function<void(size_t)>* f = &fn;
+  auto work = [st, f, n] {
+    size_t mine = 0;
+    for (;;) {
+      const size_t i = st->next.fetch_add(1);
+      if (i >= n) break;
+      try {
+        (*f)(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(st->dm);
+        if (!st->err) st->err = std::current_exception();
+      }
+      ++mine;
+    }
+    if (mine) {
+      std::lock_guard<std::mutex> g(st->dm);
+      st->done += mine;
+      if (st->done == n) st->dcv.notify_all();
+    }
+  };
+  const size_t helpers = std::min(n, ts_.size()) - (n <= ts_.size() ? 1 : 0);
   {
     std::lock_guard<std::mutex> g(mu_);
-    for (size_t i = 0; i < n; ++i)
-      q_.push_back([&, i] {
-        try {
-          fn(i);
-        } catch (...) {
-          std::lock_guard<std::mutex> g2(dm);
-          if (!err) err = std::current_exception();
-        }
-        std::lock_guard<std::mutex> g2(dm);
-        if (++done == n) dcv.notify_all();
-      });
+    for (size_t t = 0; t < helpers; ++t) q_.push_back(work);
   }
   cv_.notify_all();
-  std::unique_lock<std::mutex> l(dm);
-  dcv.wait(l, [&] { return done == n; });
-  if (err) std::rethrow_exception(err);
+  work();
+  std::unique_lock<std::mutex> l(st->dm);
+  st->dcv.wait(l, [&] { return st->done == n; });
+  if (st->err) std::rethrow_exception(st->err);
 }
 
 // --------------------------------------------------------------- plugin
@@ -482,7 +503,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
 
   if (count() < want) {
-    auto nodes = overlay_.lookup(a, (int)overlay_.nodes().size());
+    auto nodes = overlay_.lookup(a, (int)overlay_.size());
     auto from_node = [&](const std::shared_ptr<Node>& nd) {
       for (int i = 0; i < total; ++i)
         if (!have(i) && !try_node(nd, i)) return;  // down: skip the node
@@ -639,7 +660,7 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
 
 void ErasureConsensus::_remove(const Address& a) {
   if (a.mutable_block()) return backend_->remove(a);
-  for (auto& nd : overlay_.lookup(a, (int)overlay_.nodes().size()))
+  for (auto& nd : overlay_.lookup(a, (int)overlay_.size()))
     for (int i = 0; i < o_.k + o_.m; ++i) {
       try {
         nd->remove(shard_key(a, i));
@@ -733,7 +754,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
         std::set<Address> holders;
         for (int i = 0; i < total; ++i)
           if (t.pl.owner[i]) holders.insert(t.pl.owner[i]);
-        auto cand = overlay_.allocate(t.a, (int)overlay_.nodes().size());
+        auto cand = overlay_.allocate(t.a, (int)overlay_.size());
         size_t ci = 0;
         for (int r = 0; r < e; ++r) {
           const int i = t.lost[r];

@@ -32,16 +32,30 @@ Address Address::random(uint8_t fl) {
   return Address(v, fl, true);
 }
 
+// OpenSSL 3 resolves EVP_sha256() through the provider store, under a lock,
+// at every EVP_DigestInit_ex: with 16 pool threads hashing small blocks that
+// lock serialised the plugin.  The digest is fetched once, and each thread
+// reuses its own context.
+namespace {
+const EVP_MD* sha256_md() {
+  static EVP_MD* md = EVP_MD_fetch(nullptr, "SHA256", nullptr);
+  return md;
+}
+struct MdCtx {
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  ~MdCtx() { EVP_MD_CTX_free(c); }
+};
+}  // namespace
+
 std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b, size_t nb) {
   std::array<uint8_t, 32> out;
-  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  thread_local MdCtx ctx;
+  EVP_MD_CTX* c = ctx.c;
   unsigned len = 0;
-  if (!c || EVP_DigestInit_ex(c, EVP_sha256(), nullptr) != 1 || EVP_DigestUpdate(c, a, na) != 1 ||
-      (b && nb && EVP_DigestUpdate(c, b, nb) != 1) || EVP_DigestFinal_ex(c, out.data(), &len) != 1) {
-    EVP_MD_CTX_free(c);
+  const EVP_MD* md = sha256_md();
+  if (!c || !md || EVP_DigestInit_ex(c, md, nullptr) != 1 || EVP_DigestUpdate(c, a, na) != 1 ||
+      (b && nb && EVP_DigestUpdate(c, b, nb) != 1) || EVP_DigestFinal_ex(c, out.data(), &len) != 1)
     throw Error("sha256 failed");
-  }
-  EVP_MD_CTX_free(c);
   return out;
 }
 
@@ -179,21 +193,26 @@ std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo>
   auto n = std::make_shared<Node>();
   n->id = id;
   n->silo = std::move(silo);
-  std::lock_guard<std::mutex> g(mu_);
+  std::unique_lock<std::shared_mutex> g(mu_);
   nodes_.push_back(n);
+  by_id_[n->id] = n;
   return n;
 }
 
 std::shared_ptr<Node> Overlay::node(const Address& id) const {
-  std::lock_guard<std::mutex> g(mu_);
-  for (auto& n : nodes_)
-    if (n->id == id) return n;
-  return nullptr;
+  std::shared_lock<std::shared_mutex> g(mu_);
+  auto it = by_id_.find(id);
+  return it == by_id_.end() ? nullptr : it->second;
 }
 
 std::vector<std::shared_ptr<Node>> Overlay::nodes() const {
-  std::lock_guard<std::mutex> g(mu_);
+  std::shared_lock<std::shared_mutex> g(mu_);
   return nodes_;
+}
+
+size_t Overlay::size() const {
+  std::shared_lock<std::shared_mutex> g(mu_);
+  return nodes_.size();
 }
 
 namespace {

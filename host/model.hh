@@ -12,6 +12,8 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <shared_mutex>
+#include <unordered_map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -199,10 +201,13 @@ class Overlay {
   // The first n non-evicted nodes (Overlay::lookup); may include down nodes.
   std::vector<std::shared_ptr<Node>> lookup(const Address& address, int n) const;
   std::vector<std::shared_ptr<Node>> nodes() const;
+  size_t size() const;
 
  private:
-  mutable std::mutex mu_;
+  // read-mostly: lookups take the lock shared (many fetch threads at once)
+  mutable std::shared_mutex mu_;
   std::vector<std::shared_ptr<Node>> nodes_;
+  std::unordered_map<Address, std::shared_ptr<Node>, AddressHash> by_id_;
 };
 
 // -------------------------------------------------------------- consensus
