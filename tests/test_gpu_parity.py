@@ -182,6 +182,30 @@ def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
             assert np.array_equal(got[b], want), (k, m, e, b)
 
 
+def test_one_huge_ragged_block(codec, O):
+    """One 1 GiB + 7 byte block (RS(10,4): S = 107,374,208, the last data
+    shard mostly padding): encode and a 4-erasure rebuild, the whole block
+    against the oracle."""
+    k, m, B, n = 10, 4, (1 << 30) + 7, 1
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 9001, n, B, k, S)
+    want = O.encode(k, m, S, data, threads=8)
+    d = dev(data)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    codec.synchronize()
+    assert np.array_equal(host(p), want)
+    s = np.array([[3, 4, 5, 6, 7, 8, 10, 11, 12, 13]], np.uint8)
+    l = np.array([[0, 9, 1, 2]], np.uint8)
+    surv = empty(n, k * S)
+    codec.gather_shards(k, m, S, n, d, p, dev(s), surv)
+    del d
+    out = empty(n, 4 * S)
+    codec.rebuild(k, m, dev(s), surv, dev(l), out)
+    codec.synchronize()
+    assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
+
+
 def test_small_blocks_many_per_tile(codec, O):
     # 4 KiB blocks with k=16: S=256, 16 columns per block, tables for ~17
     # blocks per tile in the rebuild kernel.
