@@ -29,15 +29,37 @@ void check(int rc, const char* what) {
 
 // ------------------------------------------------------------------ codec
 Codec::Codec(int device, int contexts) {
-  for (int i = 0; i < contexts; ++i) {
-    memo_ec_ctx* c = nullptr;
-    const int rc = memo_ec_ctx_create(device, &c);
-    if (rc != MEMO_EC_OK) {
-      for (auto* p : all_) memo_ec_ctx_destroy(p);
-      throw Error(std::string("memo_ec ctx_create: ") + memo_ec_strerror(rc));
+  std::vector<int> devs;
+  if (device >= 0) {
+    devs.push_back(device);
+  } else {
+    const int nd = memo_ec_device_count();
+    for (int d = 0; d < nd; ++d) devs.push_back(d);
+    if (devs.empty()) devs.push_back(0);  // ctx_create reports the missing GPU
+  }
+  init(devs, contexts);
+}
+
+Codec::Codec(const std::vector<int>& devices, int contexts_per_device) {
+  init(devices, contexts_per_device);
+}
+
+void Codec::init(const std::vector<int>& devices, int contexts) {
+  if (devices.empty() || contexts < 1) throw Error("memo_ec: no device / context");
+  for (int id : devices) {
+    Dev d{id, {}};
+    for (int i = 0; i < contexts; ++i) {
+      memo_ec_ctx* c = nullptr;
+      const int rc = memo_ec_ctx_create(id, &c);
+      if (rc != MEMO_EC_OK) {
+        for (auto* p : all_) memo_ec_ctx_destroy(p);
+        all_.clear();
+        throw Error(std::string("memo_ec ctx_create: ") + memo_ec_strerror(rc));
+      }
+      all_.push_back(c);
+      d.free.push_back(c);
     }
-    all_.push_back(c);
-    free_.push_back(c);
+    dev_.push_back(std::move(d));
   }
 }
 
@@ -45,37 +67,65 @@ Codec::~Codec() {
   for (auto* c : all_) memo_ec_ctx_destroy(c);
 }
 
-memo_ec_ctx* Codec::acquire() {
+memo_ec_ctx* Codec::acquire(size_t d) {
   std::unique_lock<std::mutex> l(mu_);
-  cv_.wait(l, [&] { return !free_.empty(); });
-  auto* c = free_.back();
-  free_.pop_back();
+  cv_.wait(l, [&] { return !dev_[d].free.empty(); });
+  auto* c = dev_[d].free.back();
+  dev_[d].free.pop_back();
   return c;
 }
 
-void Codec::release(memo_ec_ctx* c) {
+void Codec::release(size_t d, memo_ec_ctx* c) {
   {
     std::lock_guard<std::mutex> g(mu_);
-    free_.push_back(c);
+    dev_[d].free.push_back(c);
   }
-  cv_.notify_one();
+  cv_.notify_all();
+}
+
+void Codec::split(size_t n, const std::function<int(size_t, size_t, size_t)>& fn,
+                  const char* what) {
+  const size_t D = dev_.size();
+  if (D == 1 || n < 2 * D) {
+    // one device: rotate over them so concurrent small calls spread out
+    const size_t d = D == 1 ? 0 : rr_++ % D;
+    check(fn(d, 0, n), what);
+    return;
+  }
+  std::vector<int> rc(D, MEMO_EC_OK);
+  std::vector<std::thread> ts;
+  const size_t per = (n + D - 1) / D;
+  for (size_t d = 0; d < D; ++d) {
+    const size_t b0 = d * per;
+    if (b0 >= n) break;
+    const size_t cnt = std::min(per, n - b0);
+    ts.emplace_back([&, d, b0, cnt] { rc[d] = fn(d, b0, cnt); });
+  }
+  for (auto& t : ts) t.join();
+  for (int r : rc) check(r, what);
 }
 
 void Codec::encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity) {
-  auto* c = acquire();
-  const int rc = memo_ec_encode_batch(c, k, m, S, n, data, parity, MEMO_EC_HOST);
-  release(c);
+  split(n, [&](size_t d, size_t b0, size_t cnt) {
+    auto* c = acquire(d);
+    const int rc = memo_ec_encode_batch(c, k, m, S, cnt, data + b0 * k * S, parity + b0 * m * S,
+                                        MEMO_EC_HOST);
+    release(d, c);
+    return rc;
+  }, "encode");
   ++encode_calls_;
-  check(rc, "encode");
 }
 
 void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                     const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out) {
-  auto* c = acquire();
-  const int rc = memo_ec_rebuild_batch(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, MEMO_EC_HOST);
-  release(c);
+  split(n, [&](size_t d, size_t b0, size_t cnt) {
+    auto* c = acquire(d);
+    const int rc = memo_ec_rebuild_batch(c, k, m, S, cnt, surv_idx + b0 * k, surv + b0 * k * S,
+                                         lost_idx + b0 * e, e, out + b0 * e * S, MEMO_EC_HOST);
+    release(d, c);
+    return rc;
+  }, "rebuild");
   ++rebuild_calls_;
-  check(rc, "rebuild");
 }
 
 // ---------------------------------------------------------- shard format

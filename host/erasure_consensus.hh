@@ -21,6 +21,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <functional>
 #include <future>
 #include <thread>
 
@@ -31,10 +32,16 @@ namespace memo_host {
 
 // --------------------------------------------------------------- codec
 // libmemo_ec contexts for host-memory calls.  A ctx serves one thread at a
-// time (memo_ec.h); a small pool lets concurrent fetch threads decode.
+// time (memo_ec.h); a small pool per GPU lets concurrent fetch threads
+// decode.  With several GPUs a batch of n blocks is cut into contiguous
+// block ranges, one per GPU, run by one host thread each:
+// every GPU brings its own PCIe link and HBM.
 class Codec {
  public:
+  // device >= 0: that GPU; device < 0: every GPU memo_ec_device_count() sees.
   explicit Codec(int device = 0, int contexts = 4);
+  // An explicit device list (a device may repeat: tests split over one GPU).
+  Codec(const std::vector<int>& devices, int contexts_per_device);
   ~Codec();
   Codec(const Codec&) = delete;
   Codec& operator=(const Codec&) = delete;
@@ -43,13 +50,23 @@ class Codec {
                const uint8_t* lost_idx, int e, uint8_t* out);
   uint64_t encode_calls() const { return encode_calls_; }
   uint64_t rebuild_calls() const { return rebuild_calls_; }
+  size_t devices() const { return dev_.size(); }
 
  private:
-  memo_ec_ctx* acquire();
-  void release(memo_ec_ctx* c);
+  struct Dev {
+    int id;
+    std::vector<memo_ec_ctx*> free;
+  };
+  void init(const std::vector<int>& devices, int contexts);
+  memo_ec_ctx* acquire(size_t d);
+  void release(size_t d, memo_ec_ctx* c);
+  // fn(device slot, first block, blocks) over the device partition of n
+  void split(size_t n, const std::function<int(size_t, size_t, size_t)>& fn, const char* what);
   std::mutex mu_;
   std::condition_variable cv_;
-  std::vector<memo_ec_ctx*> all_, free_;
+  std::vector<memo_ec_ctx*> all_;
+  std::vector<Dev> dev_;
+  std::atomic<size_t> rr_{0};
   std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0};
 };
 
@@ -97,7 +114,7 @@ class ThreadPool {
 // ---------------------------------------------------------------- options
 struct ErasureOptions {
   int k = 10, m = 4;
-  int device = 0;
+  int device = -1;             // < 0: every GPU the library sees
   int batch_max = 256;         // blocks per GPU encode / rebuild call
   int batch_window_us = 200;   // how long the batcher waits for company
   int threads = 16;            // peer fan-out (memo's background pool is <= 16)

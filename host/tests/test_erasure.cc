@@ -421,6 +421,44 @@ TEST(concurrent_stores_batch_on_gpu, true) {
   std::printf("  (64 concurrent stores -> %llu GPU encode calls)\n", (unsigned long long)calls);
 }
 
+// Multi-GPU split: a batch cut into per-device block
+// ranges, one host thread each, gives the single-device bytes.  The device
+// list repeats GPU 0 so the split runs on a one-GPU box.
+TEST(multi_device_split_matches_single, true) {
+  const int k = 10, m = 4, n = 37;
+  const size_t B = 30000, S = memo_ec_shard_size(B, k);
+  Buffer data(n * k * S);
+  for (size_t i = 0; i < data.size(); ++i) data[i] = (uint8_t)(i * 2654435761u >> 13);
+  Buffer p1(n * m * S), p3(n * m * S);
+  Codec one(0, 1), three(std::vector<int>{0, 0, 0}, 2);
+  CHECK(three.devices() == 3);
+  one.encode(k, m, S, n, data.data(), p1.data());
+  three.encode(k, m, S, n, data.data(), p3.data());
+  CHECK(p1 == p3);
+  // rebuild shards 0 and 12 of every block from the other k
+  std::vector<uint8_t> sidx(n * k), lidx(n * 2);
+  Buffer surv(n * k * S), o1(n * 2 * S), o3(n * 2 * S);
+  for (int b = 0; b < n; ++b) {
+    int t = 0;
+    for (int i = 0; i < k + m && t < k; ++i)
+      if (i != 0 && i != 12) {
+        sidx[b * k + t] = (uint8_t)i;
+        const uint8_t* src = i < k ? &data[(b * k + i) * S] : &p1[(b * m + i - k) * S];
+        std::memcpy(&surv[(b * k + t) * S], src, S);
+        ++t;
+      }
+    lidx[b * 2] = 0;
+    lidx[b * 2 + 1] = 12;
+  }
+  one.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), 2, o1.data());
+  three.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), 2, o3.data());
+  CHECK(o1 == o3);
+  for (int b = 0; b < n; ++b) {
+    CHECK(std::memcmp(&o1[(b * 2) * S], &data[(b * k) * S], S) == 0);
+    CHECK(std::memcmp(&o1[(b * 2 + 1) * S], &p1[(b * m + 2) * S], S) == 0);
+  }
+}
+
 // Redundancy JSON (Consensus::redundancy, Paxos.cc:2218-2225 shape).
 TEST(redundancy_json, true) {
   Net net(16, 10, 4);

@@ -89,6 +89,11 @@ typedef struct memo_ec_segment {
     uint8_t *parity;     /* device: n x m x S */
 } memo_ec_segment;
 
+/* Number of GPUs the library can use (0 without a GPU).  A node process
+ * spreads its batches over them, one ctx per device per host thread
+ * (block-index partition, no collective). */
+int memo_ec_device_count(void);
+
 /* Context on GPU `device` (its own HIP stream, device scratch). */
 int memo_ec_ctx_create(int device, memo_ec_ctx **out);
 int memo_ec_ctx_destroy(memo_ec_ctx *ctx);

@@ -418,6 +418,11 @@ extern "C" {
 
 int memo_ec_version(void) { return MEMO_EC_VERSION; }
 
+int memo_ec_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 const char* memo_ec_strerror(int code) {
   switch (code) {
     case MEMO_EC_OK: return "ok";

@@ -51,7 +51,7 @@ EXPORTS = [
     "memo_ec_rebuild_batch", "memo_ec_decode_rows", "memo_ec_encode_segments",
     "memo_ec_sha256_batch", "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards",
     "memo_ec_strerror",
-    "memo_ec_version",
+    "memo_ec_version", "memo_ec_device_count",
 ]
 
 
@@ -85,6 +85,7 @@ def _lib():
         L.memo_ec_strerror.argtypes = [c_int]
         L.memo_ec_strerror.restype = ctypes.c_char_p
         L.memo_ec_version.restype = c_int
+        L.memo_ec_device_count.restype = c_int
         _LIB = L
     return _LIB
 
