@@ -545,3 +545,44 @@ def test_concurrent_contexts_from_threads(O):
     for t in range(6):
         data = O.fill_blocks(SEED, 1000 * t + 4, n, B, k, S)
         assert np.array_equal(results[t], O.encode(k, m, S, data))
+
+
+def test_concurrent_host_calls_from_threads(O):
+    """The plugin's usage: pool threads, one ctx each, issuing host-memory
+    encode and degraded-read rebuilds of mixed sizes at once (zero-copy and
+    copy-pipeline calls interleaved), every result checked."""
+    import threading
+    from memo_amd import ec
+    k, m = 10, 4
+    cases = []
+    for i, (B, n) in enumerate([(4096, 1), (65536, 3), (1 << 20, 6), (4096, 40), (300000, 20)]):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 7000 + i, n, B, k, S)
+        par = O.encode(k, m, S, data)
+        s, l = O.erasures(SEED, 7000 + i, n, k, m, 2)
+        cases.append((S, n, data, par, s, O.gather(k, m, S, data, par, s), l,
+                      O.gather(k, m, S, data, par, l)))
+    errs = []
+
+    def work(t):
+        try:
+            with ec.Codec(0) as c:
+                for it in range(12):
+                    S, n, data, par, s, surv, l, want = cases[(t + it) % len(cases)]
+                    p = np.zeros((n, m * S), np.uint8)
+                    c.encode(k, m, data, p)
+                    if not np.array_equal(p, par):
+                        errs.append(("encode", t, it))
+                    out = np.zeros((n, 2 * S), np.uint8)
+                    c.rebuild(k, m, s, surv, l, out)
+                    if not np.array_equal(out, want):
+                        errs.append(("rebuild", t, it))
+        except Exception as ex:  # pragma: no cover
+            errs.append(ex)
+
+    ts = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs, errs
