@@ -64,10 +64,6 @@ __host__ __device__ __forceinline__ uint32_t gf_mul_t(const uint8_t* lg, const u
                                                       uint32_t a, uint32_t b) {
   return (a && b) ? ex[lg[a] + lg[b]] : 0u;
 }
-__host__ __device__ __forceinline__ uint32_t gf_inv_t(const uint8_t* lg, const uint8_t* ex,
-                                                      uint32_t a) {
-  return a ? ex[255 - lg[a]] : 0u;
-}
 
 // Copy the 1024-byte log/antilog image into LDS (256 dwords).
 __device__ __forceinline__ void stage_gf(uint32_t* s_gf) {
