@@ -9,6 +9,8 @@
 //   dma_rw : dma_r + the same stores
 //   reg_rw_staged : reg_rw with the stores regrouped through LDS (one shard per wave)
 //   write  : the 4 output shards only
+//   reg_rw1 : reg_r + one output shard (a 1-erasure rebuild's traffic)
+//   reg_rw_2tiles : reg_rw with two tiles per workgroup, all loads before all stores
 // Interleaved rounds after a warm burst (clock ramp).
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/_bin/lds_dma_probe tools/lds_dma_probe.hip
 #include <hip/hip_runtime.h>
@@ -127,6 +129,53 @@ __global__ void __launch_bounds__(256) reg_rw_staged_kernel(Geo g) {
   }
 }
 
+// reg_rw with one output shard (a 1-erasure rebuild's traffic)
+__global__ void __launch_bounds__(256) reg_rw1_kernel(Geo g) {
+  uint64_t io, oo;
+  bool valid;
+  unit_of(g, io, oo, valid);
+  u32x4 d[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j)
+    d[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(g.in + io + j * g.S));
+  u32x4 a = d[0];
+#pragma unroll
+  for (int j = 1; j < K; ++j) a ^= d[j];
+  const uint64_t b = oo / (M * g.S);
+  if (valid) __builtin_nontemporal_store(a, reinterpret_cast<u32x4*>(g.out + b * g.S + (oo - b * M * g.S)));
+}
+
+// reg_rw over two tiles per workgroup: both tiles' loads, then both tiles'
+// stores (longer read and write runs per CU)
+__global__ void __launch_bounds__(256) reg_rw_t2_kernel(Geo g) {
+  u32x4 a[2], d0[2][M];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    uint64_t u = ((uint64_t)blockIdx.x * 2 + t) * 256 + threadIdx.x;
+    if (u >= g.n * g.C) u = 0;
+    const uint64_t b = u / g.C, c = u - b * g.C;
+    const uint8_t* in = g.in + b * K * g.S + c * 16;
+    u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + j * g.S));
+      x ^= v;
+      if (j < M) d0[t][j] = v;
+    }
+    a[t] = x;
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const uint64_t u = ((uint64_t)blockIdx.x * 2 + t) * 256 + threadIdx.x;
+    if (u >= g.n * g.C) continue;
+    const uint64_t b = u / g.C, c = u - b * g.C;
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+      __builtin_nontemporal_store(a[t] ^ d0[t][i],
+                                  reinterpret_cast<u32x4*>(g.out + b * M * g.S + i * g.S + c * 16));
+  }
+}
+
 // write-only reference: the 4 output shards of every tile, nothing read
 __global__ void __launch_bounds__(256) write_kernel(Geo g) {
   uint64_t io, oo;
@@ -153,8 +202,9 @@ int main(int argc, char** argv) {
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
-  constexpr int NV = 6;
-  const char* names[NV] = {"reg_r", "dma_r", "reg_rw", "dma_rw", "reg_rw_staged", "write"};
+  constexpr int NV = 8;
+  const char* names[NV] = {"reg_r", "dma_r", "reg_rw", "dma_rw", "reg_rw_staged", "write", "reg_rw1",
+                           "reg_rw_2tiles"};
   auto launch = [&](int v) {
     switch (v) {
       case 0: hipLaunchKernelGGL(reg_kernel<false>, dim3(grid), dim3(256), 0, 0, g); break;
@@ -162,7 +212,9 @@ int main(int argc, char** argv) {
       case 2: hipLaunchKernelGGL(reg_kernel<true>, dim3(grid), dim3(256), 0, 0, g); break;
       case 3: hipLaunchKernelGGL(dma_kernel<true>, dim3(grid), dim3(256), 0, 0, g); break;
       case 4: hipLaunchKernelGGL(reg_rw_staged_kernel, dim3(grid), dim3(256), 0, 0, g); break;
-      default: hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, 0, g); break;
+      case 5: hipLaunchKernelGGL(write_kernel, dim3(grid), dim3(256), 0, 0, g); break;
+      case 6: hipLaunchKernelGGL(reg_rw1_kernel, dim3(grid), dim3(256), 0, 0, g); break;
+      default: hipLaunchKernelGGL(reg_rw_t2_kernel, dim3((grid + 1) / 2), dim3(256), 0, 0, g); break;
     }
   };
   std::vector<std::vector<float>> ms(NV);
@@ -183,7 +235,7 @@ int main(int argc, char** argv) {
   for (int v = 0; v < NV; ++v) {
     std::sort(ms[v].begin(), ms[v].end());
     const double med = ms[v][ms[v].size() / 2];
-    const double bytes = (v == 5 ? 0.0 : rbytes) + (v >= 2 ? wbytes : 0.0);
+    const double bytes = (v == 5 ? 0.0 : rbytes) + (v == 6 ? wbytes / M : v >= 2 ? wbytes : 0.0);
     printf("{\"probe\":\"%s\",\"blocks\":%llu,\"ms_med\":%.4f,\"TBs\":%.3f,\"frac\":%.4f}\n",
            names[v], (unsigned long long)n, med, bytes / (med * 1e-3) / 1e12,
            bytes / (med * 1e-3) / 8e12);
