@@ -37,6 +37,17 @@
 #define MEMO_EC_MAC_EXTRA_KC 1
 #endif
 
+// 1: rebuild tables built 4 coefficients per lane at once (packed doublings)
+#ifndef MEMO_EC_MAC_COEF4
+#define MEMO_EC_MAC_COEF4 1
+#endif
+// 1: rebuild tables in split q / lo LDS regions with one pad slot per set
+// (bank-conflict-free image stores and per-block set reads); 0: the
+// interleaved 8-dword images of the encode tables
+#ifndef MEMO_EC_MAC_COEF_SOA
+#define MEMO_EC_MAC_COEF_SOA 1
+#endif
+
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
 #endif
@@ -47,10 +58,13 @@ namespace memo_ec {
 constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
 // Fold shards pairwise (three 3-input XORs per 2 coefficients).
 constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
+constexpr bool MAC_COEF4 = MEMO_EC_MAC_COEF4 != 0;
+constexpr bool MAC_COEF_SOA = MEMO_EC_MAC_COEF_SOA != 0;
 // Table dwords per lane staged through registers ahead of the shard loads.
 constexpr int MAC_TAB_REGS = 2;
 // Coefficients per lane staged through registers (rebuild tables built in
-// LDS): 256 * 6 = 1536 = the flat-mapping LDS budget (48 KiB) / 32 B.
+// LDS): 256 * 6 = 1536 slots, the most a flat-mapped rebuild tile builds
+// (launch planning in memo_ec.cpp keeps to it).
 constexpr int MAC_COEF_REGS = 6;
 // A tile = 256 16-byte columns = one workgroup of gf_mac_kernel.
 constexpr uint32_t MAC_TILE = 256;
@@ -67,6 +81,10 @@ struct MacSeg {
   uint64_t coef_bstride;  //   coef_rows x kin bytes (tables built in LDS; tab unused);
                           //   coef_bstride 0: one set of rows for every block
   uint32_t coef_rows;
+  uint32_t coef_dense;    // 1: per-block rows are exactly R x kpad (kin == kpad, R ==
+                          //   coef_rows, coef_bstride == R * kin): slot ci of a tile is
+                          //   byte ci of its range
+  uint32_t lo_dw;         // COEF with MAC_COEF_SOA: LDS dword offset of the lo region
   uint64_t n;             // blocks
   uint64_t tiles;         // tiles (= workgroups) of this segment
   uint64_t tiles_per_block;  // aligned mapping only

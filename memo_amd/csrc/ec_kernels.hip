@@ -157,9 +157,23 @@ __device__ __forceinline__ Sel make_sel(uint32_t x) {
 struct Tab {
   uint32_t lo, m0, m1, h0, h1;
 };
-__device__ __forceinline__ Tab read_tab(const uint32_t* tp) {
-  const uint4 q = *reinterpret_cast<const uint4*>(tp);
-  return Tab{tp[4], q.x, q.y, q.z, q.w};
+// The LDS tables of one set: interleaved 8-dword images (q + 8s; encode) or
+// split q / lo regions (q + 4s, l + s; rebuild, see put_image).
+template <bool SOA>
+struct TabRef {
+  const uint32_t* q;
+  const uint32_t* l;
+};
+template <bool SOA>
+__device__ __forceinline__ Tab read_tab(const TabRef<SOA>& t, uint32_t s) {
+  if constexpr (SOA) {
+    const uint4 q = *reinterpret_cast<const uint4*>(t.q + 4 * s);
+    return Tab{t.l[s], q.x, q.y, q.z, q.w};
+  } else {
+    const uint32_t* tp = t.q + 8 * s;
+    const uint4 q = *reinterpret_cast<const uint4*>(tp);
+    return Tab{tp[4], q.x, q.y, q.z, q.w};
+  }
 }
 __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl, uint32_t& pm,
                                         uint32_t& ph) {
@@ -175,9 +189,9 @@ __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl
 // acc[i] ^= coef(i, j0 + g) * d[g] for the KC shards of one chunk.  Shards
 // are taken in pairs so that 6 partial products + the accumulator fold with
 // three 3-input XORs.  Branch-free: padded rows/shards have all-zero tables.
-template <int KC, int R>
+template <int KC, int R, bool SOA>
 __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
-                                          const uint32_t* tab, uint32_t kpad, uint32_t j0) {
+                                          const TabRef<SOA>& tab, uint32_t kpad, uint32_t j0) {
   // Pairing costs 12 selector VGPRs: the k = 16 body keeps 4 waves per
   // SIMD only without it (MEMO_EC_MAC_PAIR16).
   constexpr bool PAIR = MAC_PAIR && (KC != 16 || MEMO_EC_MAC_PAIR16);
@@ -197,10 +211,10 @@ __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d
     }
 #pragma unroll
     for (int i = 0; i < R; ++i) {
-      const uint32_t* tp = tab + (i * kpad + j0 + g) * 8;
-      const Tab ta = read_tab(tp);
+      const uint32_t sl = i * kpad + j0 + g;
+      const Tab ta = read_tab(tab, sl);
       if (two) {
-        const Tab tb = read_tab(tp + 8);
+        const Tab tb = read_tab(tab, sl + 1);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {
           uint32_t al, am, ah, bl, bm, bh;
@@ -336,28 +350,82 @@ __device__ __forceinline__ bool seg_tile(const MacLaunch& L, uint32_t& sid, uint
 }
 
 // ---- Rebuild tables built in LDS from per-block decode coefficients.
-// Product-table image of coefficient c (the layout of table_dword), from its
-// doublings d_i = c * 2^i: lo = c*{0,1,2,3}, mid = c*{0..7}<<2,
-// hi = c*{0..7}<<5.
+// Layout (MAC_COEF_SOA): the images of a tile's table sets are split into a
+// q region (mid0 mid1 hi0 hi1: 16 B per slot) and a lo region (4 B per
+// slot), each set followed by one pad slot.  Consecutive slots' image stores
+// are then bank-conflict-free (16-B / 4-B strides), and the 2-4 sets one
+// wave reads (one per block its 64 columns touch) fall in distinct banks.
+// The interleaved 32-B image of the encode tables cost the 4 KiB RS(16,4)
+// rebuild 2/3 of its LDS cycles in bank conflicts (SQ_LDS_BANK_CONFLICT,
+// DESIGN.md 4.1).  Slot x of the padded numbering (x = ci + set): q at
+// s_tab + 4x, lo at s_tab + lo_dw + x.
 __device__ __forceinline__ uint32_t gf_xtime(uint32_t x) { return (x << 1) ^ ((x >> 7) * 0x11Du); }
 __device__ __forceinline__ uint32_t pack4(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   return a | (b << 8) | (c << 16) | (d << 24);
 }
-__device__ __forceinline__ void coef_image(uint32_t c, uint32_t* dst) {
+// Product-table image of coefficient c (the layout of table_dword), from its
+// doublings d_i = c * 2^i: lo = c*{0,1,2,3}, mid = c*{0..7}<<2,
+// hi = c*{0..7}<<5.
+__device__ __forceinline__ void coef_image(uint32_t c, uint4& q, uint32_t& lo) {
   const uint32_t d0 = c, d1 = gf_xtime(d0), d2 = gf_xtime(d1), d3 = gf_xtime(d2);
   const uint32_t d4 = gf_xtime(d3), d5 = gf_xtime(d4), d6 = gf_xtime(d5), d7 = gf_xtime(d6);
-  const uint4 q = make_uint4(pack4(0, d2, d3, d2 ^ d3), pack4(d4, d4 ^ d2, d4 ^ d3, d4 ^ d3 ^ d2),
-                             pack4(0, d5, d6, d5 ^ d6), pack4(d7, d7 ^ d5, d7 ^ d6, d7 ^ d6 ^ d5));
-  *reinterpret_cast<uint4*>(dst) = q;
-  *reinterpret_cast<uint4*>(dst + 4) = make_uint4(pack4(0, d0, d1, d0 ^ d1), 0, 0, 0);
+  q = make_uint4(pack4(0, d2, d3, d2 ^ d3), pack4(d4, d4 ^ d2, d4 ^ d3, d4 ^ d3 ^ d2),
+                 pack4(0, d5, d6, d5 ^ d6), pack4(d7, d7 ^ d5, d7 ^ d6, d7 ^ d6 ^ d5));
+  lo = pack4(0, d0, d1, d0 ^ d1);
+}
+// Four images at once (byte a of c4 = coefficient a): the doublings run on 4
+// bytes per dword and v_perm transposes them into per-coefficient dwords,
+// about half the VALU work of four coef_image calls.
+__device__ __forceinline__ uint32_t gf_xtime4(uint32_t x) {
+  return ((x & 0x7f7f7f7fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1du);
+}
+// Coefficient a's [0, A_a, B_a, A_a ^ B_a] for packed A, B; one v_perm
+// interleaves two coefficients: u = [A_a, B_a, A_a+1, B_a+1].
+__device__ __forceinline__ void pair_dwords(uint32_t A, uint32_t B, uint32_t (&q)[4]) {
+  const uint32_t u01 = __builtin_amdgcn_perm(B, A, 0x05010400u);
+  const uint32_t u23 = __builtin_amdgcn_perm(B, A, 0x07030602u);
+  const uint32_t y01 = u01 ^ (u01 >> 8), y23 = u23 ^ (u23 >> 8);
+  q[0] = __builtin_amdgcn_perm(y01, u01, 0x0401000cu);
+  q[1] = __builtin_amdgcn_perm(y01, u01, 0x0603020cu);
+  q[2] = __builtin_amdgcn_perm(y23, u23, 0x0401000cu);
+  q[3] = __builtin_amdgcn_perm(y23, u23, 0x0603020cu);
+}
+__device__ __forceinline__ uint32_t bcast_byte(uint32_t x, uint32_t a) {
+  return __builtin_amdgcn_perm(x, x, a * 0x01010101u);
+}
+__device__ __forceinline__ void coef_image4(uint32_t c4, uint4 (&q)[4], uint32_t (&lo)[4]) {
+  const uint32_t d0 = c4, d1 = gf_xtime4(d0), d2 = gf_xtime4(d1), d3 = gf_xtime4(d2);
+  const uint32_t d4 = gf_xtime4(d3), d5 = gf_xtime4(d4), d6 = gf_xtime4(d5), d7 = gf_xtime4(d6);
+  uint32_t mid[4], hi[4];
+  pair_dwords(d2, d3, mid);
+  pair_dwords(d5, d6, hi);
+  pair_dwords(d0, d1, lo);
+#pragma unroll
+  for (uint32_t a = 0; a < 4; ++a)
+    q[a] = make_uint4(mid[a], mid[a] ^ bcast_byte(d4, a), hi[a], hi[a] ^ bcast_byte(d7, a));
+}
+
+// Store the image of slot ci (per = R * kpad slots per set).
+__device__ __forceinline__ void put_image(uint32_t* s_tab, const MacSeg& sg, uint32_t per,
+                                          uint32_t ci, const uint4& q, uint32_t lo) {
+  if constexpr (MAC_COEF_SOA) {
+    const uint32_t x = ci + ci / per;  // one pad slot per set
+    *reinterpret_cast<uint4*>(s_tab + 4 * x) = q;
+    s_tab[sg.lo_dw + x] = lo;
+  } else {
+    *reinterpret_cast<uint4*>(s_tab + 8 * ci) = q;
+    *reinterpret_cast<uint4*>(s_tab + 8 * ci + 4) = make_uint4(lo, 0, 0, 0);
+  }
 }
 
 // Coefficient of table-image slot ci (set, row i, column j; kpad columns per
 // row, R rows per set): rows[b_first + set][i][j] for i < coef_rows, j < kin,
-// else 0 (padding).
+// else 0 (padding).  coef_dense: the rows are exactly R x kpad, so slot ci is
+// byte ci of the tile's range.
 template <int R>
 __device__ __forceinline__ uint32_t coef_at(const MacSeg& sg, const Unit& u, uint32_t ci,
                                             uint32_t kpad) {
+  if (sg.coef_dense) return sg.coef[u.b_first * sg.coef_bstride + ci];
   const uint32_t set = ci / (R * kpad), rem = ci - set * (R * kpad);
   const uint32_t i = rem / kpad, j = rem - i * kpad;
   if (i >= sg.coef_rows || j >= sg.kin) return 0u;
@@ -371,7 +439,9 @@ __device__ __forceinline__ uint32_t coef_sets(const MacSeg& sg, const Unit& u) {
 }
 
 // Register-staged coefficient loads for the hot path (issued before the
-// shard loads; vmcnt retires in order), then the images into LDS.
+// shard loads; vmcnt retires in order), then the images into LDS.  Lane t
+// owns slots t + 256q, so each image store instruction covers consecutive
+// slots.
 template <int R, int KP>
 __device__ __forceinline__ void load_coefs(const MacSeg& sg, const Unit& u,
                                            uint32_t (&cv)[MAC_COEF_REGS]) {
@@ -386,18 +456,50 @@ template <int R, int KP>
 __device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
                                              const uint32_t (&cv)[MAC_COEF_REGS], uint32_t* s_tab) {
   const uint32_t total = coef_sets(sg, u) * (R * KP);
+  const uint32_t t = threadIdx.x;
+  if constexpr (MAC_COEF4) {
+    static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
+    if (t < total) {  // waves past the tile's slots skip the build
+      uint4 q[4];
+      uint32_t lo[4];
+      coef_image4(pack4(cv[0], cv[1], cv[2], cv[3]), q, lo);
 #pragma unroll
-  for (int q = 0; q < MAC_COEF_REGS; ++q) {
-    const uint32_t ci = threadIdx.x + 256u * q;
-    if (ci < total) coef_image(cv[q], s_tab + ci * 8);
+      for (uint32_t a = 0; a < 4; ++a)
+        if (t + 256u * a < total) put_image(s_tab, sg, R * KP, t + 256u * a, q[a], lo[a]);
+    }
+    if (t + 1024u < total) {
+      uint4 q[4];
+      uint32_t lo[4];
+      coef_image4(pack4(cv[4], cv[5], 0, 0), q, lo);
+#pragma unroll
+      for (uint32_t a = 0; a < 2; ++a)
+        if (t + 256u * (4 + a) < total) put_image(s_tab, sg, R * KP, t + 256u * (4 + a), q[a], lo[a]);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < MAC_COEF_REGS; ++k) {
+      const uint32_t ci = t + 256u * k;
+      if (ci < total) {
+        uint4 q;
+        uint32_t lo;
+        coef_image(cv[k], q, lo);
+        put_image(s_tab, sg, R * KP, ci, q, lo);
+      }
+    }
   }
 }
+
 // Unstaged variant (generic chunk loop, runtime kpad).
 template <int R>
 __device__ __forceinline__ void stage_images(const MacSeg& sg, const Unit& u, uint32_t* s_tab) {
-  const uint32_t total = coef_sets(sg, u) * (R * sg.kpad);
-  for (uint32_t ci = threadIdx.x; ci < total; ci += 256)
-    coef_image(coef_at<R>(sg, u, ci, sg.kpad), s_tab + ci * 8);
+  const uint32_t per = R * sg.kpad;
+  const uint32_t total = coef_sets(sg, u) * per;
+  for (uint32_t ci = threadIdx.x; ci < total; ci += 256) {
+    uint4 q;
+    uint32_t lo;
+    coef_image(coef_at<R>(sg, u, ci, sg.kpad), q, lo);
+    put_image(s_tab, sg, per, ci, q, lo);
+  }
 }
 
 // One tile of segment sg: KC is the straight-line shard chunk (kin == KC is
@@ -410,8 +512,17 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   const uint32_t set_dw = R * kpad * 8;
 
   const Unit u = locate(sg, tile);
-  const bool per_block = COEF ? sg.coef_bstride != 0 : sg.tab_bstride != 0;
-  const uint32_t* tab = s_tab + (per_block ? u.set * set_dw : 0u);
+  constexpr bool SOA = COEF && MAC_COEF_SOA;
+  TabRef<SOA> tab;
+  if constexpr (SOA) {
+    const uint32_t x0 = sg.coef_bstride ? u.set * (R * kpad + 1) : 0u;  // padded slot of set
+    tab.q = s_tab + 4 * x0;
+    tab.l = s_tab + sg.lo_dw + x0;
+  } else {
+    const bool per_block = COEF ? sg.coef_bstride != 0 : sg.tab_bstride != 0;
+    tab.q = s_tab + (per_block ? u.set * set_dw : 0u);
+    tab.l = nullptr;
+  }
   uint32_t acc[R][4];
 #pragma unroll
   for (int i = 0; i < R; ++i)

@@ -111,21 +111,32 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   s.out_bstride = out_bs; s.out_sstride = out_ss;
   s.tab_bstride = tab_bs_dw;
   s.coef = coef; s.coef_bstride = coef_bs; s.coef_rows = coef_rows;
+  s.coef_dense = coef && coef_bs != 0 && coef_rows == (uint32_t)R &&
+                 kin == kpad_of(kin, KC) && coef_bs == (uint64_t)R * kin;
   s.n = n; s.kin = kin; s.r = r;
   s.kpad = kpad_of(kin, KC);
   s.chunks = (uint32_t)(S / 16);
-  const size_t set_bytes = (size_t)R * s.kpad * 32;
+  // LDS per table set: 8-dword images, or (rebuild, MAC_COEF_SOA) 16-B q +
+  // 4-B lo per slot plus one pad slot (ec_kernels.hip: put_image)
+  const size_t per = (size_t)R * s.kpad;
+  const bool soa = coef != nullptr && MAC_COEF_SOA;
+  const size_t set_bytes = soa ? (per + 1) * 20 : per * 32;
   const uint64_t C = s.chunks;
+  uint64_t sets;
   if (coef ? coef_bs == 0 : tab_bs_dw == 0) {  // one table set for every block
     s.flat = 1;
-    p.lds = set_bytes;
-  } else if (sets_per_tile(C) * set_bytes <= kLdsBudget) {
+    sets = 1;
+  } else if (sets_per_tile(C) * set_bytes <= kLdsBudget &&
+             (!coef || sets_per_tile(C) * per <= 256u * MAC_COEF_REGS)) {
+    // (the hot path stages at most MAC_COEF_REGS coefficients per lane)
     s.flat = 1;
-    p.lds = sets_per_tile(C) * set_bytes;
+    sets = sets_per_tile(C);
   } else {
     s.flat = 0;
-    p.lds = set_bytes;
+    sets = 1;
   }
+  p.lds = sets * set_bytes;
+  s.lo_dw = soa ? (uint32_t)(sets * (per + 1) * 4) : 0u;
   if (s.flat) {
     s.tiles = (n * C + MAC_TILE - 1) / MAC_TILE;
     s.tiles_per_block = 0;
