@@ -5,11 +5,74 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <set>
 
 namespace memo_host {
 
 namespace {
+
+// MEMO_EC_PLUGIN_TIMING=1: per-phase wall times of the batched paths on
+// stderr (profiling the host side; off by default).
+struct PhaseTimer {
+  const char* what;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  std::string line;
+  explicit PhaseTimer(const char* w) : what(w) {
+    static const bool env = [] {
+      const char* p = std::getenv("MEMO_EC_PLUGIN_TIMING");
+      return p && *p == '1';
+    }();
+    on = env;
+    t = std::chrono::steady_clock::now();
+  }
+  void lap(const char* phase) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    line += std::string(" ") + phase + "=" +
+            std::to_string(std::chrono::duration<double, std::milli>(now - t).count()) + "ms";
+    t = now;
+  }
+  ~PhaseTimer() {
+    if (on) std::fprintf(stderr, "[timing] %s%s\n", what, line.c_str());
+  }
+};
+
+// Batch scratch whose bytes are all written before they are read: a vector
+// that default-initialises (no zero fill of hundreds of MB on one thread;
+// the padding is zeroed where it is written).
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = NoInitAlloc<U>;
+  };
+  NoInitAlloc() = default;
+  template <class U>
+  NoInitAlloc(const NoInitAlloc<U>&) {}
+  template <class U>
+  void construct(U* p) noexcept {
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using Scratch = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
+
+// Block payload d as k shards of Sb bytes into k slots of S >= Sb bytes at
+// dst (memo_ec_shard_size padding and the slot tails zeroed).
+void copy_padded(const Buffer& d, int k, size_t Sb, uint8_t* dst, size_t S) {
+  for (int j = 0; j < k; ++j) {
+    const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
+    uint8_t* slot = dst + (size_t)j * S;
+    if (hi > lo) std::memcpy(slot, d.data() + lo, hi - lo);
+    std::memset(slot + (hi - lo), 0, S - (hi - lo));
+  }
+}
 // Batches mix shard sizes within a power-of-two bucket: every byte column is
 // coded independently, so a shard zero-padded to the batch's largest S codes
 // exactly (the tail codes to zero and is dropped); padding stays below 2x.
@@ -144,7 +207,10 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
 
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   if (h.salt.size() > 32) throw Error("shard: salt longer than 32 bytes");
-  Buffer w(ShardHeader::kSize + h.shard_size, 0);
+  Buffer w;
+  w.reserve(ShardHeader::kSize + h.shard_size);
+  w.resize(ShardHeader::kSize, 0);
+  w.insert(w.end(), payload, payload + h.shard_size);
   std::memcpy(w.data(), "MECS", 4);
   w[4] = h.version;
   w[5] = h.k;
@@ -156,9 +222,8 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   const uint32_t sl = (uint32_t)h.salt.size();
   std::memcpy(w.data() + 56, &sl, 4);
   if (sl) std::memcpy(w.data() + 60, h.salt.data(), sl);
-  const uint32_t crc = crc32c(payload, h.shard_size);
+  const uint32_t crc = crc32c(w.data() + ShardHeader::kSize, h.shard_size);
   std::memcpy(w.data() + 92, &crc, 4);
-  std::memcpy(w.data() + ShardHeader::kSize, payload, h.shard_size);
   return w;
 }
 
@@ -305,7 +370,7 @@ std::string ErasureConsensus::redundancy() const {
 std::string ErasureConsensus::stats() const {
   size_t blocks;
   {
-    std::lock_guard<std::mutex> g(index_mu_);
+    std::shared_lock<std::shared_mutex> g(index_mu_);
     blocks = index_.size();
   }
   return to_json({{"blocks", std::to_string(blocks)},
@@ -350,14 +415,10 @@ void ErasureConsensus::batcher_loop() {
       size_t S = 0;
       for (auto* j : g.second) S = std::max(S, memo_ec_shard_size(j->block->data.size(), o_.k));
       try {
-        Buffer data(n * o_.k * S, 0), parity(n * o_.m * S);
+        Scratch data(n * o_.k * S), parity(n * o_.m * S);
         for (size_t i = 0; i < n; ++i) {
           const auto& d = g.second[i]->block->data;
-          const size_t Sb = memo_ec_shard_size(d.size(), o_.k);
-          for (int j = 0; j < o_.k; ++j) {
-            const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
-            std::copy(d.begin() + lo, d.begin() + hi, data.begin() + (i * o_.k + j) * S);
-          }
+          copy_padded(d, o_.k, memo_ec_shard_size(d.size(), o_.k), data.data() + i * o_.k * S, S);
         }
         codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
         for (size_t i = 0; i < n; ++i) {
@@ -376,10 +437,16 @@ void ErasureConsensus::batcher_loop() {
 }
 
 // Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360).
-void ErasureConsensus::place(const Block& b, const Buffer& parity, bool parallel) {
+void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstride,
+                             const uint8_t* data, size_t dstride, bool parallel) {
   const int total = o_.k + o_.m;
   const size_t S = memo_ec_shard_size(b.data.size(), o_.k);
-  const Buffer data = padded(b, S);
+  Buffer own;
+  if (!data) {  // the block's own shards, zero-padded
+    own = padded(b, S);
+    data = own.data();
+    dstride = S;
+  }
   auto owners = overlay_.allocate(b.address, total);
   if ((int)owners.size() < o_.k)
     throw TooFewPeers("erasure: " + std::to_string(owners.size()) + " reachable owners, need " +
@@ -398,7 +465,7 @@ void ErasureConsensus::place(const Block& b, const Buffer& parity, bool parallel
     h.shard_size = S;
     h.address = b.address;
     h.salt = b.salt;
-    const uint8_t* p = i < (size_t)o_.k ? data.data() + i * S : parity.data() + (i - o_.k) * S;
+    const uint8_t* p = i < (size_t)o_.k ? data + i * dstride : parity + (i - o_.k) * pstride;
     try {
       owners[i]->store(shard_key(b.address, (int)i), encode_shard(h, p));
       ok[i] = 1;
@@ -415,7 +482,7 @@ void ErasureConsensus::place(const Block& b, const Buffer& parity, bool parallel
       ++reached;
     }
   {
-    std::lock_guard<std::mutex> g(index_mu_);
+    std::unique_lock<std::shared_mutex> g(index_mu_);
     index_[b.address] = pl;
   }
   if (reached < o_.k)
@@ -434,7 +501,8 @@ void ErasureConsensus::_store(const Block& b, StoreMode mode) {
     bq_.push_back(&job);
   }
   bcv_.notify_all();
-  place(b, fut.get());
+  const Buffer parity = fut.get();
+  place(b, parity.data(), memo_ec_shard_size(b.data.size(), o_.k), nullptr, 0);
 }
 
 void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
@@ -448,11 +516,13 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
   // encode is one GPU call per shard-size bucket.
   for (size_t b0 = 0; b0 < imm.size(); b0 += o_.batch_max) {
     const size_t n0 = std::min<size_t>(o_.batch_max, imm.size() - b0);
+    PhaseTimer tm("store_many");
     std::vector<char> valid(n0, 0);
     pool_.parallel_for(n0, [&](size_t i) {
       const Block* b = imm[b0 + i];
       valid[i] = chb_valid(b->address, b->salt, b->data);
     });
+    tm.lap("chb");
     std::map<int, std::vector<const Block*>> by_s;
     for (size_t i = 0; i < n0; ++i) {
       const Block* b = imm[b0 + i];
@@ -463,24 +533,22 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
       const size_t n = g.second.size();
       size_t S = 0;
       for (auto* b : g.second) S = std::max(S, memo_ec_shard_size(b->data.size(), o_.k));
-      Buffer data(n * o_.k * S, 0), parity(n * o_.m * S);
+      Scratch data(n * o_.k * S), parity(n * o_.m * S);
+      tm.lap("alloc");
       pool_.parallel_for(n, [&](size_t i) {
         const auto& d = g.second[i]->data;
-        const size_t Sb = memo_ec_shard_size(d.size(), o_.k);
-        for (int j = 0; j < o_.k; ++j) {
-          const size_t lo = std::min(d.size(), (size_t)j * Sb), hi = std::min(d.size(), (size_t)(j + 1) * Sb);
-          std::copy(d.begin() + lo, d.begin() + hi, data.begin() + (i * o_.k + j) * S);
-        }
+        copy_padded(d, o_.k, memo_ec_shard_size(d.size(), o_.k), data.data() + i * o_.k * S, S);
       });
+      tm.lap("copy_in");
       codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
+      tm.lap("encode");
+      // shards straight from the batch buffers (a block's shard is the first
+      // Sb bytes of its S-byte slot)
       pool_.parallel_for(n, [&](size_t i) {
-        const size_t Sb = memo_ec_shard_size(g.second[i]->data.size(), o_.k);
-        Buffer p((size_t)o_.m * Sb);
-        for (int r = 0; r < o_.m; ++r)
-          std::copy(parity.begin() + (i * o_.m + r) * S, parity.begin() + (i * o_.m + r) * S + Sb,
-                    p.begin() + (size_t)r * Sb);
-        place(*g.second[i], p, /*parallel=*/false);  // already on the pool
+        place(*g.second[i], parity.data() + i * o_.m * S, S, data.data() + i * o_.k * S, S,
+              /*parallel=*/false);  // already on the pool
       });
+      tm.lap("place");
     }
   }
 }
@@ -496,8 +564,13 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
                                                                     ShardHeader* hdr,
                                                                     bool parallel) {
   const int total = o_.k + o_.m;
+  // shard keys (a SHA-256 each) are derived when a pass first needs them,
+  // always outside the parallel fetches: the data shards' first
   std::vector<Key> keys(total);
-  for (int i = 0; i < total; ++i) keys[i] = shard_key(a, i);
+  int keyed = 0;
+  auto key_upto = [&](int n) {
+    for (; keyed < n; ++keyed) keys[keyed] = shard_key(a, keyed);
+  };
   std::map<int, Buffer> got;
   std::mutex gm;
   any_down = false;
@@ -538,7 +611,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
 
   std::vector<std::shared_ptr<Node>> owner(total);
   {
-    std::lock_guard<std::mutex> g(index_mu_);
+    std::shared_lock<std::shared_mutex> g(index_mu_);
     auto it = index_.find(a);
     if (it != index_.end())
       for (int i = 0; i < total && i < (int)it->second.owner.size(); ++i)
@@ -546,6 +619,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
   for (int pass = 0; pass < 2 && count() < want; ++pass) {
     // pass 0: the data shards (no decode needed); pass 1: the parity shards
+    key_upto(pass ? total : o_.k);
     std::vector<int> ids;
     for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i)
       if (owner[i] && !owner[i]->evicted && !have(i)) ids.push_back(i);
@@ -553,6 +627,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
 
   if (count() < want) {
+    key_upto(total);
     auto nodes = overlay_.lookup(a, (int)overlay_.size());
     auto from_node = [&](const std::shared_ptr<Node>& nd) {
       for (int i = 0; i < total; ++i)
@@ -662,8 +737,10 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       errs[i] = std::current_exception();
     }
   }
+  PhaseTimer tm("fetch_many");
   std::vector<Gathered> g(n);
   pool_.parallel_for(imm.size(), [&](size_t t) { g[imm[t]] = collect(addresses[imm[t]], false); });
+  tm.lap("gather");
   std::map<std::pair<int, size_t>, std::vector<size_t>> groups;
   std::vector<size_t> direct;
   for (size_t i : imm) {
@@ -682,6 +759,7 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
     }
   };
   pool_.parallel_for(direct.size(), [&](size_t t) { finish(direct[t], nullptr, 0); });
+  tm.lap("assemble_direct");
   for (auto& grp : groups) {
     const int e = (int)grp.first.second;
     auto& ids = grp.second;
@@ -690,19 +768,24 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
       for (size_t bi = 0; bi < nb; ++bi) S = std::max(S, (size_t)g[ids[b0 + bi]].h.shard_size);
       std::vector<uint8_t> sidx(nb * k), lidx(nb * e);
-      Buffer surv(nb * k * S, 0), out(nb * e * S);
+      Scratch surv(nb * k * S), out(nb * e * S);
+      tm.lap("alloc");
       pool_.parallel_for(nb, [&](size_t bi) {
         Gathered& x = g[ids[b0 + bi]];
         for (int s = 0; s < k; ++s) {
           sidx[bi * k + s] = (uint8_t)x.shards[s].first;
-          std::memcpy(surv.data() + (bi * k + s) * S, x.shards[s].second.data() + ShardHeader::kSize,
-                      x.h.shard_size);
+          uint8_t* slot = surv.data() + (bi * k + s) * S;
+          std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
+          std::memset(slot + x.h.shard_size, 0, S - x.h.shard_size);
         }
         std::copy(x.lost.begin(), x.lost.end(), lidx.begin() + bi * e);
       });
+      tm.lap("copy_in");
       codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data());
+      tm.lap("rebuild");
       decoded_ += nb;
       pool_.parallel_for(nb, [&](size_t bi) { finish(ids[b0 + bi], out.data() + bi * e * S, S); });
+      tm.lap("assemble");
     }
   }
   for (size_t i = 0; i < n; ++i) res(addresses[i], std::move(blocks[i]), errs[i]);
@@ -717,7 +800,7 @@ void ErasureConsensus::_remove(const Address& a) {
       } catch (Error&) {
       }
     }
-  std::lock_guard<std::mutex> g(index_mu_);
+  std::unique_lock<std::shared_mutex> g(index_mu_);
   index_.erase(a);
 }
 
@@ -733,7 +816,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
   // first so the scan does not hold its lock)
   std::vector<Todo> all;
   {
-    std::lock_guard<std::mutex> g(index_mu_);
+    std::shared_lock<std::shared_mutex> g(index_mu_);
     all.reserve(index_.size());
     for (auto& kv : index_) all.push_back(Todo{kv.first, kv.second, {}, {}});
   }
@@ -771,7 +854,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
       size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
       for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(g.second[b0 + bi]->pl.B, k));
       std::vector<uint8_t> sidx(n * k), lidx(n * e);
-      Buffer surv(n * k * S, 0), out(n * e * S);
+      Scratch surv(n * k * S), out(n * e * S);
       std::vector<int> good(n, 1);
       pool_.parallel_for(n, [&](size_t bi) {
         Todo& t = *g.second[b0 + bi];
@@ -781,7 +864,9 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
             auto wire = overlay_.node(t.pl.owner[i])->fetch(shard_key(t.a, i));
             const uint8_t* p = nullptr;
             const ShardHeader h = decode_shard(wire, &p);
-            std::memcpy(surv.data() + (bi * k + s) * S, p, h.shard_size);
+            uint8_t* slot = surv.data() + (bi * k + s) * S;
+            std::memcpy(slot, p, h.shard_size);
+            std::memset(slot + h.shard_size, 0, S - h.shard_size);
             sidx[bi * k + s] = (uint8_t)i;
           } catch (Error&) {
             good[bi] = 0;
@@ -833,7 +918,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
       for (size_t bi = 0; bi < n; ++bi) {
         if (!good[bi]) continue;
         Todo& t = *g.second[b0 + bi];
-        std::lock_guard<std::mutex> lk(index_mu_);
+        std::unique_lock<std::shared_mutex> lk(index_mu_);
         index_[t.a] = t.pl;
         ++rep.blocks_repaired;
         rep.shards_rebuilt += (size_t)e;

@@ -172,7 +172,10 @@ class ErasureConsensus : public StackedConsensus {
                                   size_t stride);
   Buffer padded(const Block& b, size_t S) const;
   // parallel = false stores the shards one by one (callers on the pool).
-  void place(const Block& b, const Buffer& parity, bool parallel = true);
+  // Shard i of b to owner i: data shard j at data + j*dstride (nullptr: b's
+  // own zero-padded payload), parity shard r at parity + r*pstride.
+  void place(const Block& b, const uint8_t* parity, size_t pstride, const uint8_t* data,
+             size_t dstride, bool parallel = true);
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);
@@ -181,7 +184,7 @@ class ErasureConsensus : public StackedConsensus {
   ErasureOptions o_;
   Codec codec_;
   ThreadPool pool_;
-  mutable std::mutex index_mu_;
+  mutable std::shared_mutex index_mu_;  // readers: fetch paths; writers: place, repair, remove
   std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_node_blocks analogue
   // batcher (host C++ batching of concurrent stores into one GPU call)
   std::mutex bmu_;

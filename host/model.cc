@@ -118,39 +118,52 @@ bool MemorySilo::_contains(const Key& k) const {
 }
 
 bool MemorySilo::_try_get(const Key& k, Buffer& out) const {
-  std::lock_guard<std::mutex> g(mu_);
-  auto it = blocks_.find(k);
-  if (it == blocks_.end()) return false;
-  out = it->second;
+  std::shared_ptr<const Buffer> v;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = blocks_.find(k);
+    if (it == blocks_.end()) return false;
+    v = it->second;
+  }
+  out = *v;
   return true;
 }
 
 Buffer MemorySilo::_get(const Key& k) const {
-  std::lock_guard<std::mutex> g(mu_);
-  auto it = blocks_.find(k);
-  if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
-  return it->second;
+  std::shared_ptr<const Buffer> v;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    auto it = blocks_.find(k);
+    if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
+    v = it->second;
+  }
+  return *v;
 }
 
 int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
+  auto nv = std::make_shared<const Buffer>(v);  // the copy, outside the lock
+  std::shared_ptr<const Buffer> old;            // freed outside the lock
   std::lock_guard<std::mutex> g(mu_);
   auto it = blocks_.find(k);
   if (it == blocks_.end()) {
     if (!insert) throw silo::MissingKey("missing key " + k.hex());
-    blocks_.emplace(k, v);
+    blocks_.emplace(k, std::move(nv));
     return (int)v.size();
   }
   if (!update) throw silo::Collision("key exists " + k.hex());
-  const int delta = (int)v.size() - (int)it->second.size();
-  it->second = v;
+  const int delta = (int)v.size() - (int)it->second->size();
+  old = std::move(it->second);
+  it->second = std::move(nv);
   return delta;
 }
 
 int MemorySilo::_erase(const Key& k) {
+  std::shared_ptr<const Buffer> old;
   std::lock_guard<std::mutex> g(mu_);
   auto it = blocks_.find(k);
   if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
-  const int delta = -(int)it->second.size();
+  const int delta = -(int)it->second->size();
+  old = std::move(it->second);
   blocks_.erase(it);
   return delta;
 }

@@ -160,8 +160,10 @@ class MemorySilo : public Silo {
   std::vector<Key> _list() override;
 
  private:
+  // Values are immutable once stored: readers take a reference under the
+  // lock and copy outside it, writers copy before taking it.
   mutable std::mutex mu_;
-  std::map<Key, Buffer> blocks_;
+  std::map<Key, std::shared_ptr<const Buffer>> blocks_;
 };
 
 // ------------------------------------------------------------ peers/overlay
