@@ -390,7 +390,7 @@ def main():
                                  ("pageable", (hd.numpy().copy(), np.zeros((ne, m * S), np.uint8)))]:
             codec.encode(k, m, src, dst)
             t = time.perf_counter()
-            reps = 3
+            reps = 6
             for _ in range(reps):
                 codec.encode(k, m, src, dst)
             el = time.perf_counter() - t

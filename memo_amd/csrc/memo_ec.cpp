@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -243,25 +244,95 @@ constexpr int kSlots = 3;
 
 // Pageable <-> pinned bounce copies run on several host threads: one thread
 // moves ~10-20 GB/s, below the ~50 GB/s a PCIe Gen5 x16 direction carries.
-void par_memcpy(void* dst, const void* src, size_t n) {
-  constexpr size_t kMin = 8u << 20;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t nt = std::min<size_t>({8, hw, n / kMin});
-  if (nt <= 1) {
-    std::memcpy(dst, src, n);
-    return;
+// The workers are shared by every ctx of the process and started once; the
+// calling thread copies a chunk too and helps with queued chunks while it
+// waits.  MEMO_EC_COPY_THREADS (read per call) caps the threads per copy;
+// 1 copies on the calling thread only.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool();  // never destroyed: workers may be blocked at exit
+    return *p;
   }
-  std::vector<std::thread> ts;
-  const size_t per = (n / nt + 63) & ~(size_t)63;
-  for (size_t t = 1; t < nt; ++t) {
-    const size_t lo = t * per;
-    if (lo >= n) break;
-    const size_t len = std::min(per, n - lo);
-    ts.emplace_back([=] { std::memcpy((char*)dst + lo, (const char*)src + lo, len); });
+  void copy(void* dst, const void* src, size_t n) {
+    constexpr size_t kChunkMin = 128u << 10;
+    size_t nt = std::min<size_t>(workers_ + 1, n / kChunkMin);
+    if (const char* p = std::getenv("MEMO_EC_COPY_THREADS"))
+      nt = std::min<size_t>(nt, (size_t)std::max(1L, std::strtol(p, nullptr, 10)));
+    if (nt <= 1) {
+      std::memcpy(dst, src, n);
+      return;
+    }
+    const size_t per = (n / nt + 63) & ~(size_t)63;
+    Job job;
+    std::vector<Chunk> mine;
+    for (size_t lo = per; lo < n; lo += per)
+      mine.push_back({(char*)dst + lo, (const char*)src + lo, std::min(per, n - lo), &job});
+    job.left = mine.size();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& c : mine) q_.push_back(c);
+    }
+    cv_.notify_all();
+    std::memcpy(dst, src, std::min(per, n));
+    // help with queued chunks (this copy's or another's) until ours are done
+    for (;;) {
+      Chunk c;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (q_.empty()) break;
+        c = q_.back();
+        q_.pop_back();
+      }
+      run(c);
+    }
+    std::unique_lock<std::mutex> l(job.m);
+    job.cv.wait(l, [&] { return job.left == 0; });
   }
-  std::memcpy(dst, src, std::min(per, n));
-  for (auto& th : ts) th.join();
-}
+
+ private:
+  struct Job {
+    std::mutex m;
+    std::condition_variable cv;
+    size_t left = 0;
+  };
+  struct Chunk {
+    char* d;
+    const char* s;
+    size_t n;
+    Job* job;
+  };
+  CopyPool() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    workers_ = std::min<unsigned>(7, hw > 1 ? hw - 1 : 0);
+    for (unsigned i = 0; i < workers_; ++i) std::thread([this] { worker(); }).detach();
+  }
+  // The job's owner returns only after taking job->m, which the last runner
+  // holds until it has notified: the job outlives every access to it.
+  static void run(const Chunk& c) {
+    std::memcpy(c.d, c.s, c.n);
+    std::lock_guard<std::mutex> g(c.job->m);
+    if (--c.job->left == 0) c.job->cv.notify_all();
+  }
+  void worker() {
+    for (;;) {
+      Chunk c;
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return !q_.empty(); });
+        c = q_.back();
+        q_.pop_back();
+      }
+      run(c);
+    }
+  }
+  unsigned workers_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Chunk> q_;
+};
+
+void par_memcpy(void* dst, const void* src, size_t n) { CopyPool::get().copy(dst, src, n); }
 
 int sync_pipeline(memo_ec_ctx* ctx) {
   for (auto st : {ctx->sh, ctx->sk, ctx->sd}) HIPCHK(hipStreamSynchronize(st));
@@ -576,13 +647,13 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
     const uint8_t* src = data;
     uint8_t* dst = parity;
     if (!pinned) {
-      std::memcpy(c->h_slot[0], data, n * in_b);
+      par_memcpy(c->h_slot[0], data, n * in_b);
       src = c->h_slot[0];
       dst = c->h_slot[0] + n * in_b;
     }
     if (int rc = encode_device(c, k, m, S, n, src, dst, c->sk)) return rc;
     HIPCHK(hipStreamSynchronize(c->sk));
-    if (!pinned) std::memcpy(parity, dst, n * out_b);
+    if (!pinned) par_memcpy(parity, dst, n * out_b);
     return MEMO_EC_OK;
   }
   size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
@@ -670,14 +741,14 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
     const uint8_t* sv = surv;
     uint8_t* ov = out;
     if (!pinned) {
-      std::memcpy(h, surv, n * in_b);
+      par_memcpy(h, surv, n * in_b);
       sv = h;
       ov = h + n * in_b;
     }
     if (int rc = rebuild_device(c, k, m, S, n, h_sidx, sv, h_lidx, e, ov, c->d_tabs, c->sk, h_st))
       return rc;
     HIPCHK(hipStreamSynchronize(c->sk));
-    if (!pinned) std::memcpy(out, ov, n * out_b);
+    if (!pinned) par_memcpy(out, ov, n * out_b);
     int drc = c->deferred;
     c->deferred = 0;
     if (drc == MEMO_EC_OK && (__atomic_load_n(h_st, __ATOMIC_ACQUIRE) & 1u)) drc = MEMO_EC_ESINGULAR;
