@@ -1,20 +1,34 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident RS(k,m) block erasure coding on MI355X.
 
-Workload (BASELINE.json configs[1], "C2"): RS(10,4) encode of 4096 x 1 MiB
-synthetic blocks per GPU, inputs resident in HBM before the timed region.
-A "step" = one encode pass over the whole batch (one kernel launch).  With
---gpus N (torchrun, one process per GPU) every rank encodes its own 4096
-blocks (block-index partition, BASELINE.json C4 at N=8): weak scaling, no
-collective on the data path -- only the timing barrier / max-over-ranks.
+Metric (BASELINE.json): GiB/s of RS(k,m) encode+rebuild over device-resident
+batched blocks, with the kernels' fraction of the HBM roofline.
+
+A "step" is one pass of the hot path over the batch in both directions:
+  * encode  -- BASELINE.json configs[1] (C2): RS(10,4) parity of 4096 x 1 MiB
+               synthetic blocks (one gf_mac_kernel launch);
+  * rebuild -- configs[2] (C3): the same 4096 blocks rebuilt from k of their
+               k+m shards with 4 random shards lost per block
+               (decode_coef_kernel rows, then gf_mac_kernel).
+Inputs are resident in HBM before the timed region.  `value` = payload bytes
+encoded + payload bytes rebuilt, over all ranks, / the job's wall time.
+
+--gpus N: one process per GPU.  Without an external launcher (WORLD_SIZE
+unset) bench.py starts the N ranks itself before touching any GPU; under
+torch.distributed.run it uses the launcher's ranks.  Every rank encodes and
+rebuilds its own 4096 blocks (block-index partition; BASELINE.json C4 at N=8):
+weak scaling.  The barrier and the max-over-ranks run over gloo on the host;
+nothing crosses GPUs (no RCCL).
 
 Printed JSON line (rank 0): the contract fields plus
-  roofline     : dominant kernel (gf_mac_kernel) algorithmic HBM bytes per
-                 launch, (k+m)*S*n, / its average HIP-event duration, vs 8 TB/s
-  cpu_baseline : the C oracle (scalar, table-driven) on this host's cores,
-                 same workload bytes, bounded sample (rank 0, N=1 only)
-  rebuild      : BASELINE.json C3 (RS(10,4), 4 random erasures per block)
-  end_to_end   : pinned host -> HBM -> host rate (PCIe-inclusive; not `value`)
+  encode / rebuild : per-direction GiB/s, kernel ms and roofline fraction
+  roofline         : the encode kernel (C2, the north-star target): its
+                     algorithmic bytes per launch (k+m)*S*n / its average
+                     HIP-event duration, vs 8 TB/s; roofline_rebuild likewise
+  ranks            : per-GPU GiB/s, node sum (C4's wording)
+  cpu_baseline     : the C port (oracle/, test infrastructure) timed on this
+                     host's cores on a bounded sample (rank 0, N=1 only)
+  end_to_end       : pinned host -> HBM -> host rate (PCIe-inclusive; not `value`)
 """
 import argparse
 import json
@@ -32,19 +46,21 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec, GB/s (MI355X_MICROARCH.md)
 METRIC = "GiB/s RS(k,m) encode+rebuild, device-resident batched blocks; % HBM roofline"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # ~60 ms of back-to-back launches: the MI355X's clocks dip a few launches
-    # into a burst and take ~40 launches to settle (profiles/r01_clock_ramp.jsonl)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=60)
+    ap.add_argument("--steps", type=int, default=25)
+    ap.add_argument("--warmup", type=int, default=30)
+    # The MI355X's clocks dip a few launches into a burst and take ~40 ms of
+    # back-to-back launches to settle (profiles/r01_clock_ramp.jsonl): untimed
+    # steps continue past --warmup until this much wall time has gone by.
+    ap.add_argument("--settle-ms", type=float, default=150.0)
     ap.add_argument("--k", type=int, default=10)
     ap.add_argument("--m", type=int, default=4)
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
     ap.add_argument("--blocks", type=int, default=4096, help="blocks per GPU")
     ap.add_argument("--erasures", type=int, default=4)
-    ap.add_argument("--no-rebuild", action="store_true")
+    ap.add_argument("--no-small", action="store_true", help="skip the 4 KiB random-rebuild lines")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -52,46 +68,56 @@ def parse():
     ap.add_argument("--sha", action="store_true",
                     help="also time GPU SHA-256 (CHB addresses) of the batch and of 4 KiB blocks")
     ap.add_argument("--sweep-gib", type=float, default=4.0, help="payload GiB per sweep point")
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (RCCL) or gloo (rehearsal)")
     ap.add_argument("--same-device", action="store_true",
-                    help="every rank on cuda:0 (rehearse N>1 on a 1-GPU box with gloo)")
-    return ap.parse_args()
+                    help="every rank on cuda:0 (rehearse N>1 on a 1-GPU box)")
+    return ap.parse_args(argv)
 
 
-def timed_launches(torch, fn, steps, warmup, dist, stream):
-    """Warmup, then exactly `steps` launches bracketed by barrier+sync; per-
-    launch HIP events on `stream` (the stream the kernels are enqueued on)."""
-    for _ in range(warmup):
-        fn()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+def timed_steps(torch, fns, steps, warmup, settle_ms, dist, stream):
+    """`warmup` untimed steps (continued until settle_ms of wall time has gone
+    by), then exactly `steps` steps bracketed by barrier + synchronize.  A
+    step runs fns in order; HIP events on `stream` (the stream the kernels
+    are enqueued on) bracket each fn.  Returns (wall seconds, per-fn lists of
+    per-step ms, untimed steps run)."""
     t0 = time.perf_counter()
-    for a, b in ev:
-        a.record(stream)
-        fn()
-        b.record(stream)
+    done = 0
+    while done < warmup or (time.perf_counter() - t0) * 1e3 < settle_ms:
+        for f in fns:
+            f()
+        done += 1
+        if done % 8 == 0:
+            torch.cuda.synchronize()  # keep the host from queueing far ahead
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    wall = time.perf_counter() - t0
-    kms = [a.elapsed_time(b) for a, b in ev]
-    return wall, kms
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(len(fns) + 1)] for _ in range(steps)]
+    t = time.perf_counter()
+    for es in ev:
+        es[0].record(stream)
+        for f, e in zip(fns, es[1:]):
+            f()
+            e.record(stream)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t
+    ms = [[es[i].elapsed_time(es[i + 1]) for es in ev] for i in range(len(fns))]
+    return wall, ms, done
 
 
-def max_over_ranks(torch, dist, x):
-    if dist is None:
-        return x
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def kstats(kms, alg_bytes):
+    """Kernel-time summary of one direction: HIP-event ms per launch and the
+    algorithmic-byte roofline fraction of the average launch."""
+    avg = float(np.mean(kms))
+    achieved = alg_bytes / (avg * 1e-3) / 1e9
+    return {"kernel_ms_avg": round(avg, 4), "kernel_ms_min": round(min(kms), 4),
+            "kernel_ms_median": round(float(np.median(kms)), 4),
+            "kernel_ms_first_last": [round(kms[0], 4), round(kms[-1], 4)],
+            "achieved": round(achieved, 1), "frac": round(achieved / PEAK_HBM_GBS, 4)}
 
 
-def sweep(torch, ec, codec, stream, gib, steps, warmup):
+def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms):
     """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
     ~gib GiB of payload per point, one encode launch per step; then the same
     12 smaller groups as ONE memo_ec_encode_segments call (one launch per
@@ -105,7 +131,8 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup):
             d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
             p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
             codec.fill_blocks(SEED, 0, n, B, k, S, d)
-            _, kms = timed_launches(torch, lambda: codec.encode(k, m, d, p), steps, warmup, None, stream)
+            _, (kms,), _ = timed_steps(torch, [lambda: codec.encode(k, m, d, p)], steps, warmup,
+                                       settle_ms, None, stream)
             ms = float(np.mean(kms))
             alg = (k + m) * S * n
             points.append({"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
@@ -123,7 +150,8 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup):
             segs.append((k, m, S, n, d, p))
             alg += (k + m) * S * n
             pay += n * B
-    _, kms = timed_launches(torch, lambda: codec.encode_segments(segs), steps, warmup, None, stream)
+    _, (kms,), _ = timed_steps(torch, [lambda: codec.encode_segments(segs)], steps, warmup,
+                               settle_ms, None, stream)
     ms = float(np.mean(kms))
     fused = {"segments": len(segs), "kernel_ms": round(ms, 4),
              "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
@@ -134,10 +162,11 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup):
             "points": points, "fused": fused}
 
 
-def rebuild_small(torch, ec, codec, stream, steps, warmup):
+def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
     """Small-block rebuild: 4 KiB blocks (~4 GiB of payload), 4 random
     erasures per block, so every block has its own decode rows and a
-    256-column tile spans up to 17 blocks' tables.  Step = decode + MAC."""
+    256-column tile spans up to 17 blocks.  Encode of the same blocks is
+    timed beside it (same process, same clocks)."""
     res = {}
     for (k, m) in [(10, 4), (16, 4)]:
         B, n, e = 4096, 1 << 20, 4
@@ -152,19 +181,21 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup):
         codec.gather_shards(k, m, S, n, d, p, sd, surv)
         want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
         codec.gather_shards(k, m, S, n, d, p, ld, want)
-        del d, p
         out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
-        _, kms = timed_launches(torch, lambda: codec.rebuild(k, m, sd, surv, ld, out),
-                                max(1, steps // 2), warmup, None, stream)
+        _, (ekms, rkms), _ = timed_steps(
+            torch, [lambda: codec.encode(k, m, d, p), lambda: codec.rebuild(k, m, sd, surv, ld, out)],
+            steps, warmup, settle_ms, None, stream)
         codec.synchronize()
-        ms = float(np.mean(kms))
+        ms = float(np.mean(rkms))
         alg = (k + e) * S * n
         res["RS(%d,%d)" % (k, m)] = {
             "blocks": n, "block_bytes": B, "shard_bytes": S, "erasures": e,
             "step_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
             "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "encode_frac_same_blocks": round((k + m) * S * n / (float(np.mean(ekms)) * 1e-3) / 1e9
+                                             / PEAK_HBM_GBS, 4),
             "bit_exact": bool(torch.equal(out, want))}
-        del surv, out, want, sd, ld
+        del d, p, surv, out, want, sd, ld
     return res
 
 
@@ -179,20 +210,26 @@ def _rate(fn, nbytes, seconds):
             return passes * nbytes / el / 2**30, passes, el
 
 
+def host_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
     """Time the CPU codecs of oracle/ on this host, on a bounded sample of
     the same workload, and cross-check them against the GPU parity of the
     same blocks.  `value` is the vectorised encode (oracle/rs_simd.c:
     GFNI+AVX-512 affine or AVX2 split-nibble, ISA-L's published x86
-    techniques), the strongest CPU codec here; the scalar table oracle is
-    reported beside it.  Test infrastructure, never the product."""
+    techniques), the strongest CPU codec here, on 16 threads (the GPU box's
+    CPU share per GPU); every core the process may run on is timed beside it
+    (`all_cores`), and the scalar table oracle too.  Test infrastructure,
+    never the product."""
     from oracle import oracle as O
     O.build()
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))  # the GPU box's CPU share is 16 per GPU
+    cores = host_cores()
+    threads = max(1, min(cores, 16))
     nb = 128
     data = O.aligned_empty((nb, k * S))
     data[:] = O.fill_blocks(SEED, 0, nb, B, k, S)
@@ -205,15 +242,27 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                           nb * B, seconds)
     one, _, _ = _rate(lambda: O.encode_simd(k, m, S, data[:64], threads=1, isa=isa, out=par[:64]),
                       64 * B, 1.5)
+    # every affinity core, one block per thread per pass (at least 128 blocks)
+    nball = max(nb, cores)
+    if nball > nb:
+        dall = O.aligned_empty((nball, k * S))
+        dall[:] = np.resize(data, (nball, k * S))
+        pall = O.aligned_empty((nball, m * S))
+    else:
+        dall, pall = data, par
+    va, _, _ = _rate(lambda: O.encode_simd(k, m, S, dall, threads=cores, isa=isa, out=pall),
+                     nball * B, 3.0)
     sc_all, _, _ = _rate(lambda: O.encode(k, m, S, data[:32], threads=threads), 32 * B, 2.0)
     sc_one, _, _ = _rate(lambda: O.encode(k, m, S, data[:2], threads=1), 2 * B, 1.0)
     return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": "RS(%d,%d) encode, %d x %d-byte blocks x %d passes (%.1f s), vectorised C port "
-                      "(%s, streaming stores) on %d threads; 1-core %.3f GiB/s; scalar table oracle "
-                      "%.3f GiB/s on %d threads, %.3f on 1; bit-exact vs GPU on %d blocks: %s"
-                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, one, sc_all, threads,
-                         sc_one, nchk, ok_simd and ok_scalar),
+                      "(%s, streaming stores) on %d threads; all %d affinity cores %.3f GiB/s; "
+                      "1-core %.3f GiB/s; scalar table oracle %.3f GiB/s on %d threads, %.3f on 1; "
+                      "bit-exact vs GPU on %d blocks: %s"
+                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, cores, va, one, sc_all,
+                         threads, sc_one, nchk, ok_simd and ok_scalar),
             "isa": O.SIMD_ISA[isa], "single_core": round(one, 3),
+            "all_cores": {"cores": cores, "value": round(va, 3), "blocks": nball},
             "scalar_oracle": {"value": round(sc_all, 3), "single_core": round(sc_one, 3)},
             "bit_exact_vs_gpu": ok_simd and ok_scalar}
 
@@ -221,23 +270,20 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
 def c1_case(torch, ec, codec, stream):
     """BASELINE.json configs[0] (C1): RS(3,2) encode + rebuild (e = 1 and 2
     random erasures per block) of 1000 x 64 KiB blocks.  The CPU oracle
-    (scalar, all host threads; the reference-runnable case) is timed beside
+    (scalar, 16 host threads; the reference-runnable case) is timed beside
     the GPU on the same bytes, and every rebuilt shard is compared across
     the two (whole batch, bit-exact)."""
     from oracle import oracle as O
     k, m, B, n = 3, 2, 65536, 1000
     S = ec.shard_size(B, k)
-    try:
-        threads = max(1, min(len(os.sched_getaffinity(0)), 16))
-    except AttributeError:
-        threads = 1
+    threads = max(1, min(host_cores(), 16))
     data = O.fill_blocks(SEED, 0, n, B, k, S)
     t0 = time.perf_counter()
     par = O.encode(k, m, S, data, threads=threads)
     cpu_enc = time.perf_counter() - t0
     d = torch.from_numpy(data).cuda()
     p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
-    _, ek = timed_launches(torch, lambda: codec.encode(k, m, d, p), 20, 20, None, stream)
+    _, (ek,), _ = timed_steps(torch, [lambda: codec.encode(k, m, d, p)], 20, 20, 0, None, stream)
     ok = bool(np.array_equal(p.cpu().numpy(), par))
     out = {"workload": "RS(3,2) encode + rebuild (e=1, e=2), 1000 x 65536-byte blocks (BASELINE.json C1)",
            "cpu_threads": threads, "cpu_kind": "port (scalar table oracle)",
@@ -250,7 +296,8 @@ def c1_case(torch, ec, codec, stream):
         cpu_reb = time.perf_counter() - t0
         sd, ld, sv = (torch.from_numpy(x).cuda() for x in (s_idx, l_idx, surv))
         o = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
-        _, rk = timed_launches(torch, lambda: codec.rebuild(k, m, sd, sv, ld, o), 20, 20, None, stream)
+        _, (rk,), _ = timed_steps(torch, [lambda: codec.rebuild(k, m, sd, sv, ld, o)], 20, 20, 0,
+                                  None, stream)
         codec.synchronize()
         ok = ok and bool(np.array_equal(o.cpu().numpy(), want))
         out["rebuild_e%d" % e] = {"cpu_ms": round(cpu_reb * 1e3, 3),
@@ -259,25 +306,169 @@ def c1_case(torch, ec, codec, stream):
     return out
 
 
+def end_to_end(torch, ec, codec, data, par, k, m, B, n):
+    """PCIe-inclusive rates (blocks start and end in host memory: RPC socket
+    in, silos/peers out); 3-stage pipeline, 64 MiB batches.  Never `value`."""
+    S = ec.shard_size(B, k)
+    ne = min(n, 1024)
+    hd = torch.empty((ne, k * S), dtype=torch.uint8).pin_memory()
+    hp = torch.empty((ne, m * S), dtype=torch.uint8).pin_memory()
+    hd.copy_(data[:ne].cpu())
+    codec.set_stream(None)
+    e2e = {}
+    for kind, (src, dst) in [("pinned", (hd, hp)),
+                             ("pageable", (hd.numpy().copy(), np.zeros((ne, m * S), np.uint8)))]:
+        codec.encode(k, m, src, dst)
+        t = time.perf_counter()
+        reps = 6
+        for _ in range(reps):
+            codec.encode(k, m, src, dst)
+        el = time.perf_counter() - t
+        ok = bool(np.array_equal(np.asarray(dst[:4]), par[:4].cpu().numpy()))
+        e2e[kind] = {"value": round(reps * ne * B / el / 2**30, 3), "bit_exact": ok}
+    res = {"workload": "RS(%d,%d) encode, %d x %d-byte blocks from host memory, parity back to "
+                       "host memory (HtoD + kernel + DtoH, 3-stage stream pipeline)" % (k, m, ne, B),
+           "unit": "GiB/s", "pinned": e2e["pinned"], "pageable": e2e["pageable"]}
+    # One-block host calls, as the plugin issues them for a lone store or a
+    # degraded read (pageable elle::Buffer in, out): latency, not rate.
+    lat = {}
+    for bb in (4096, B):
+        Sb = ec.shard_size(bb, k)
+        d1 = np.frombuffer(np.random.default_rng(1).bytes(k * Sb), np.uint8).reshape(1, -1).copy()
+        p1 = np.zeros((1, m * Sb), np.uint8)
+        s1 = np.arange(1, k + 1, dtype=np.uint8).reshape(1, k)
+        l1 = np.zeros((1, 1), np.uint8)
+        o1 = np.zeros((1, Sb), np.uint8)
+        for name, fn in (("encode", lambda: codec.encode(k, m, d1, p1)),
+                         ("rebuild_e1", lambda: codec.rebuild(k, m, s1, d1, l1, o1))):
+            for _ in range(20):
+                fn()
+            ts = []
+            for _ in range(200):
+                t = time.perf_counter()
+                fn()
+                ts.append(time.perf_counter() - t)
+            lat["%s_%dB_us" % (name, bb)] = round(float(np.median(ts)) * 1e6, 1)
+    lat["note"] = ("median of 200 one-block calls from pageable host memory (copy in, kernels, "
+                   "copy out, synchronous), RS(%d,%d)" % (k, m))
+    return res, lat
+
+
+def sha_lines(torch, codec, stream, data, n, B):
+    import hashlib
+    res = {}
+    for name, nb, bb in [("C2 batch, 1 MiB blocks", n, B), ("4 KiB blocks", 1 << 20, 4096)]:
+        msg = data if bb == B else torch.empty((nb, bb), dtype=torch.uint8, device="cuda")
+        stride = msg.shape[1]
+        if bb != B:
+            codec.fill_blocks(SEED, 0, nb, bb, 1, bb, msg)
+        pre = torch.zeros((nb, 64), dtype=torch.uint8, device="cuda")  # salt || owner
+        dig = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
+        fn = lambda: codec.sha256(msg, dig, prefix=pre, uniform_len=bb, msg_stride=stride)  # noqa
+        _, (kms,), _ = timed_steps(torch, [fn], 5, 1, 0, None, stream)
+        ms = float(np.mean(kms))
+        ok = dig[0].cpu().numpy().tobytes() == hashlib.sha256(
+            bytes(64) + msg[0, :bb].cpu().numpy().tobytes()).digest()
+        one = msg[0, :bb].cpu().numpy().tobytes()
+        t = time.perf_counter()
+        reps = max(1, (64 << 20) // bb)
+        for _ in range(reps):
+            hashlib.sha256(one).digest()
+        cpu = reps * bb / (time.perf_counter() - t) / 1e9
+        res[name] = {"blocks": nb, "block_bytes": bb, "kernel_ms": round(ms, 3),
+                     "GBs": round(nb * (bb + 64) / (ms * 1e-3) / 1e9, 1), "bit_exact": ok,
+                     "cpu_1core_GBs": round(cpu, 2)}
+        if bb != B:
+            del msg
+    return {"workload": "batched SHA-256(salt||owner||data) = CHB addresses (CHB.cc:264-289), "
+                        "one lane per block", **res}
+
+
+def assemble(args, world, rows, wall_max, S):
+    """The contract line from the ranks' rows (pure: tested on CPU)."""
+    from memo_amd.partition import node_report
+    k, m, B, n, e, K = args.k, args.m, args.block_bytes, args.blocks, args.erasures, args.steps
+    r0 = rows[0]
+    step_payload = n * B * (2 if e > 0 else 1)
+    value = world * step_payload * K / wall_max / 2**30
+    enc_alg = (k + m) * S * n
+    enc = r0["encode"]
+    roof = {"bound": "hbm", "kernel": "gf_mac_kernel (encode)", "achieved": enc["achieved"],
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": enc["frac"], "traffic": None,
+            "bytes_per_launch": enc_alg,
+            "read_only_frac": round(k * S * n / (enc["kernel_ms_avg"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            **{x: enc[x] for x in ("kernel_ms_avg", "kernel_ms_min", "kernel_ms_median",
+                                   "kernel_ms_first_last")},
+            "kernel_ms_max_over_ranks": round(max(r["encode"]["kernel_ms_avg"] for r in rows), 4)}
+    res = {
+        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
+        "steps": K, "warmup": args.warmup, "ms_per_step": round(wall_max / K * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": "RS(%d,%d) encode (BASELINE.json C2) + rebuild with %d random erasures "
+                               "per block (C3) of %d x %d-byte blocks per GPU%s; step = one encode "
+                               "launch + one rebuild launch" % (k, m, e, n, B,
+                                                                "" if world == 1 else " (C4 at N=8)"),
+                   "k": k, "m": m, "block_bytes": B, "blocks_per_gpu": n, "shard_bytes": S,
+                   "erasures": e, "global_blocks": n * world,
+                   "parallelism": "block-index partition x%d, no collective on data" % world},
+        "roofline": roof,
+        "warmup_steps_run": r0["warmup_steps_run"],
+        "encode": {"value": round(world * n * B * K / wall_max / 2**30, 3) if e <= 0 else None,
+                   "GiBs_kernel": round(n * B / (enc["kernel_ms_avg"] * 1e-3) / 2**30, 1), **enc},
+    }
+    if e > 0:
+        reb = r0["rebuild"]
+        rb_alg = (k + e) * S * n
+        res["encode"].pop("value")
+        res["rebuild"] = {"GiBs_kernel": round(n * B / (reb["kernel_ms_avg"] * 1e-3) / 2**30, 1),
+                          "bytes_per_launch": rb_alg, "round_trip_bit_exact": all(
+                              r["rebuild_bit_exact"] for r in rows), **reb}
+        res["roofline_rebuild"] = {"bound": "hbm", "kernel": r0["rebuild_kernel"],
+                                   "achieved": reb["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                                   "frac": reb["frac"], "traffic": None, "bytes_per_launch": rb_alg,
+                                   "kernel_ms_avg": reb["kernel_ms_avg"]}
+    per = [{"rank": r["rank"], "device": r["device"], "payload_bytes": r["payload_bytes"],
+            "seconds": r["device_seconds"]} for r in rows]
+    rep = node_report(per)
+    res["ranks"] = {"per_gpu": [{"rank": r["rank"], "device": r["device"],
+                                 "GiBs": rep["per_gpu_GiBs"][i],
+                                 "encode_kernel_ms": r["encode"]["kernel_ms_avg"],
+                                 "encode_frac": r["encode"]["frac"],
+                                 **({"rebuild_kernel_ms": r["rebuild"]["kernel_ms_avg"],
+                                     "rebuild_frac": r["rebuild"]["frac"]} if e > 0 else {})}
+                                for i, r in enumerate(rows)],
+                    "node_sum_GiBs": rep["node_sum_GiBs"],
+                    "note": "per-GPU GiB/s = that rank's payload / its own kernel time (HIP events); "
+                            "node sum = all payload / the slowest rank's kernel time; `value` = all "
+                            "payload / the job's wall time between barriers"}
+    return res
+
+
 def main():
     args = parse()
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # Start the N ranks here, before anything touches a GPU (children,
+        # never an exec), one per device; each rank re-enters main().
+        from memo_amd.partition import launch_local_ranks
+        sys.exit(launch_local_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
+                                    same_device=args.same_device))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    import torch
     dist = None
-    if args.same_device:
-        local = 0
     if world > 1:
         import torch.distributed as dist_mod
-        torch.cuda.set_device(local)
-        if args.dist_backend == "nccl":
-            dist_mod.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist_mod.init_process_group(args.dist_backend)
+        # gloo on the host: the barrier and the max/gather of timings only
+        dist_mod.init_process_group("gloo")
         dist = dist_mod
-    else:
-        torch.cuda.set_device(0)
+    if torch.cuda.device_count() <= local:
+        raise SystemExit("bench.py: rank %d needs cuda:%d, %d visible" % (rank, local,
+                                                                          torch.cuda.device_count()))
+    torch.cuda.set_device(local)
     from memo_amd import ec
     from memo_amd.partition import weak_range
 
@@ -287,7 +478,7 @@ def main():
     # events that time each launch are recorded on the same stream.
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    codec = ec.Codec(local if world > 1 else 0)
+    codec = ec.Codec(local)
     codec.set_stream(stream)
     assert codec.stream == stream.cuda_stream and stream.cuda_stream
 
@@ -295,58 +486,9 @@ def main():
     par = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
     first_block, _ = weak_range(n, rank)  # rank r owns blocks [r*n, (r+1)*n)
     codec.fill_blocks(SEED, first_block, n, B, k, S, data)
-    torch.cuda.synchronize()
-
-    enc = lambda: codec.encode(k, m, data, par)  # noqa: E731
-    wall, kms = timed_launches(torch, enc, args.steps, args.warmup, dist, stream)
-    codec.synchronize()
-    wall = max_over_ranks(torch, dist, wall)
-    kavg_ms = float(np.mean(kms))
-    kavg_ms_max = max_over_ranks(torch, dist, kavg_ms)
-    payload = world * n * B * args.steps
-    value = payload / wall / 2**30
-    alg_bytes = (k + m) * S * n
-    achieved = alg_bytes / (kavg_ms * 1e-3) / 1e9
-
-    result = {
-        "metric": METRIC, "value": round(value, 3), "unit": "GiB/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "RS(%d,%d) encode, %d x %d-byte blocks per GPU (BASELINE.json %s)"
-                               % (k, m, n, B, "C2" if world == 1 else "C4"),
-                   "k": k, "m": m, "block_bytes": B, "blocks_per_gpu": n, "shard_bytes": S,
-                   "global_blocks": n * world, "parallelism": "block-index partition x%d" % world},
-        "roofline": {"bound": "hbm", "kernel": "gf_mac_kernel", "achieved": round(achieved, 1),
-                     "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": round(achieved / PEAK_HBM_GBS, 4),
-                     "traffic": None, "bytes_per_launch": alg_bytes,
-                     "kernel_ms_avg": round(kavg_ms, 4), "kernel_ms_min": round(min(kms), 4),
-                     "kernel_ms_median": round(float(np.median(kms)), 4),
-                     "kernel_ms_first_last": [round(kms[0], 4), round(kms[-1], 4)],
-                     "kernel_ms_max_over_ranks": round(kavg_ms_max, 4),
-                     "read_only_frac": round(k * S * n / (kavg_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)},
-    }
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            t = json.load(open(pmc))
-            key = "encode_%d_%d_%d_%d" % (k, m, B, n)
-            if key in t:
-                result["roofline"]["traffic"] = t[key]["hbm_bytes_per_launch"]
-                result["roofline"]["traffic_source"] = t[key]["source"]
-        except Exception:
-            pass
-
-    # Measured HBM reference on this box: a device-to-device
-    # copy of the same data bytes on the same stream (read + write).
-    scratch = torch.empty_like(data)
-    _, cms = timed_launches(torch, lambda: scratch.copy_(data), 10, 30, None, stream)
-    copy_gbs = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
-    result["roofline"]["copy_GBs"] = round(copy_gbs, 1)
-    result["roofline"]["frac_of_copy"] = round(achieved / copy_gbs, 4)
-    del scratch
-
-    if not args.no_rebuild and e > 0:
+    fns = [lambda: codec.encode(k, m, data, par)]
+    if e > 0:
+        codec.encode(k, m, data, par)
         s_idx, l_idx = ec.erasures(SEED, first_block, n, k, m, e)
         sd = torch.from_numpy(s_idx).cuda()
         ld = torch.from_numpy(l_idx).cuda()
@@ -355,118 +497,73 @@ def main():
         out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
         want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
         codec.gather_shards(k, m, S, n, data, par, ld, want)
-        reb = lambda: codec.rebuild(k, m, sd, surv, ld, out)  # noqa: E731
-        rwall, rkms = timed_launches(torch, reb, max(1, args.steps // 2), args.warmup, dist, stream)
-        codec.synchronize()
-        ok = bool(torch.equal(out, want))
-        rwall = max_over_ranks(torch, dist, rwall)
-        rsteps = max(1, args.steps // 2)
-        rk = float(np.mean(rkms))
-        rbytes = (k + e) * S * n
-        result["rebuild"] = {
-            "workload": "RS(%d,%d) rebuild, %d random erasures/block, %d x %d-byte blocks per GPU "
-                        "(BASELINE.json C3)" % (k, m, e, n, B),
-            "value": round(world * n * B * rsteps / rwall / 2**30, 3), "unit": "GiB/s",
-            "ms_per_step": round(rwall / rsteps * 1e3, 4),
-            "step_ms_events": round(rk, 4),
-            "achieved_GBs": round(rbytes / (rk * 1e-3) / 1e9, 1),
-            "frac": round(rbytes / (rk * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-            "note": "step = decode_coef_kernel (closed-form decode rows) + gf_mac_kernel",
-            "round_trip_bit_exact": ok}
+        fns.append(lambda: codec.rebuild(k, m, sd, surv, ld, out))
+    torch.cuda.synchronize()
+
+    wall, kms, done = timed_steps(torch, fns, args.steps, args.warmup, args.settle_ms, dist, stream)
+    codec.synchronize()
+    row = {"rank": rank, "device": local, "warmup_steps_run": done,
+           "payload_bytes": n * B * len(fns) * args.steps,
+           "device_seconds": sum(sum(x) for x in kms) * 1e-3,
+           "encode": kstats(kms[0], (k + m) * S * n)}
+    if e > 0:
+        row["rebuild"] = kstats(kms[1], (k + e) * S * n)
+        row["rebuild_bit_exact"] = bool(torch.equal(out, want))
+        row["rebuild_kernel"] = ec.rebuild_kernel_name()
         del surv, out, want
-        if world == 1:
-            result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps, args.warmup)
+    rows = [row]
+    wall_max = wall
+    if dist is not None:
+        rows = [None] * world
+        dist.all_gather_object(rows, row)
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall_max = float(t.item())
+    result = assemble(args, world, rows, wall_max, S)
 
-    if not args.no_e2e and world == 1:
-        # PCIe-inclusive: blocks start and end in host memory (RPC socket in,
-        # silos/peers out).  3-stage pipeline, 64 MiB batches; never `value`.
-        ne = min(n, 1024)
-        hd = torch.empty((ne, k * S), dtype=torch.uint8).pin_memory()
-        hp = torch.empty((ne, m * S), dtype=torch.uint8).pin_memory()
-        hd.copy_(data[:ne].cpu())
-        codec.set_stream(None)
-        e2e = {}
-        for kind, (src, dst) in [("pinned", (hd, hp)),
-                                 ("pageable", (hd.numpy().copy(), np.zeros((ne, m * S), np.uint8)))]:
-            codec.encode(k, m, src, dst)
-            t = time.perf_counter()
-            reps = 6
-            for _ in range(reps):
-                codec.encode(k, m, src, dst)
-            el = time.perf_counter() - t
-            ok = bool(np.array_equal(np.asarray(dst[:4]), par[:4].cpu().numpy()))
-            e2e[kind] = {"value": round(reps * ne * B / el / 2**30, 3), "bit_exact": ok}
-        result["end_to_end"] = {
-            "workload": "RS(%d,%d) encode, %d x %d-byte blocks from host memory, parity back to "
-                        "host memory (HtoD + kernel + DtoH, 3-stage stream pipeline)" % (k, m, ne, B),
-            "unit": "GiB/s", "pinned": e2e["pinned"], "pageable": e2e["pageable"]}
-        # One-block host calls, as the plugin issues them for a lone store or
-        # a degraded read (pageable elle::Buffer in, out): latency, not rate.
-        lat = {}
-        for bb in (4096, B):
-            Sb = ec.shard_size(bb, k)
-            d1 = np.frombuffer(np.random.default_rng(1).bytes(k * Sb), np.uint8).reshape(1, -1).copy()
-            p1 = np.zeros((1, m * Sb), np.uint8)
-            s1 = np.arange(1, k + 1, dtype=np.uint8).reshape(1, k)
-            l1 = np.zeros((1, 1), np.uint8)
-            o1 = np.zeros((1, Sb), np.uint8)
-            for name, fn in (("encode", lambda: codec.encode(k, m, d1, p1)),
-                             ("rebuild_e1", lambda: codec.rebuild(k, m, s1, d1, l1, o1))):
-                for _ in range(20):
-                    fn()
-                ts = []
-                for _ in range(200):
-                    t = time.perf_counter()
-                    fn()
-                    ts.append(time.perf_counter() - t)
-                lat["%s_%dB_us" % (name, bb)] = round(float(np.median(ts)) * 1e6, 1)
-        result["host_call_latency"] = dict(
-            lat, note="median of 200 one-block calls from pageable host memory (copy in, kernels, "
-                      "copy out, synchronous), RS(%d,%d)" % (k, m))
-        codec.set_stream(stream)
+    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc):
+        try:
+            t = json.load(open(pmc))
+            for key, obj in (("encode_%d_%d_%d_%d" % (k, m, B, n), result["roofline"]),
+                             ("rebuild_%d_%d_%d_%d_e%d" % (k, m, B, n, e), result.get("roofline_rebuild"))):
+                if obj is not None and key in t:
+                    obj["traffic"] = t[key]["hbm_bytes_per_launch"]
+                    obj["traffic_source"] = t[key]["source"]
+        except (OSError, ValueError, KeyError):
+            pass
 
-    if rank == 0 and world == 1 and not args.no_cpu:
-        sample = par[:4].cpu().numpy()
-        result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, sample)
-        result["c1"] = c1_case(torch, ec, codec, stream)
-
-    if args.sha and world == 1:
-        import hashlib
-        res = {}
-        for name, nb, bb in [("C2 batch, 1 MiB blocks", n, B), ("4 KiB blocks", 1 << 20, 4096)]:
-            msg = data if bb == B else torch.empty((nb, bb), dtype=torch.uint8, device="cuda")
-            stride = msg.shape[1]
-            if bb != B:
-                codec.fill_blocks(SEED, 0, nb, bb, 1, bb, msg)
-            pre = torch.zeros((nb, 64), dtype=torch.uint8, device="cuda")  # salt || owner
-            dig = torch.empty((nb, 32), dtype=torch.uint8, device="cuda")
-            fn = lambda: codec.sha256(msg, dig, prefix=pre, uniform_len=bb, msg_stride=stride)  # noqa
-            _, kms = timed_launches(torch, fn, 5, 1, None, stream)
-            ms = float(np.mean(kms))
-            ok = dig[0].cpu().numpy().tobytes() == hashlib.sha256(
-                bytes(64) + msg[0, :bb].cpu().numpy().tobytes()).digest()
-            one = msg[0, :bb].cpu().numpy().tobytes()
-            t = time.perf_counter()
-            reps = max(1, (64 << 20) // bb)
-            for _ in range(reps):
-                hashlib.sha256(one).digest()
-            cpu = reps * bb / (time.perf_counter() - t) / 1e9
-            res[name] = {"blocks": nb, "block_bytes": bb, "kernel_ms": round(ms, 3),
-                         "GBs": round(nb * (bb + 64) / (ms * 1e-3) / 1e9, 1), "bit_exact": ok,
-                         "cpu_1core_GBs": round(cpu, 2)}
-            if bb != B:
-                del msg
-        result["sha256"] = {"workload": "batched SHA-256(salt||owner||data) = CHB addresses "
-                                        "(CHB.cc:264-289), one lane per block", **res}
-
-    if args.sweep and world == 1:
-        del data, par
-        result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4), args.warmup)
+    if world == 1:
+        # Measured HBM reference on this box: a device-to-
+        # device copy of the same data bytes on the same stream (read + write).
+        scratch = torch.empty_like(data)
+        _, (cms,), _ = timed_steps(torch, [lambda: scratch.copy_(data)], 10, 30, 0, None, stream)
+        copy_gbs = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
+        result["roofline"]["copy_GBs"] = round(copy_gbs, 1)
+        result["roofline"]["frac_of_copy"] = round(result["roofline"]["achieved"] / copy_gbs, 4)
+        del scratch
+        if not args.no_small:
+            result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps,
+                                                    args.warmup, args.settle_ms)
+        if not args.no_e2e:
+            result["end_to_end"], result["host_call_latency"] = end_to_end(
+                torch, ec, codec, data, par, k, m, B, n)
+            codec.set_stream(stream)
+        if not args.no_cpu:
+            result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, par[:4].cpu().numpy())
+            result["c1"] = c1_case(torch, ec, codec, stream)
+        if args.sha:
+            result["sha256"] = sha_lines(torch, codec, stream, data, n, B)
+        if args.sweep:
+            del data, par
+            result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4),
+                                    args.warmup, args.settle_ms)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
     codec.close()
     if dist is not None:
+        dist.barrier()
         dist.destroy_process_group()
 
 

@@ -192,8 +192,8 @@ void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
 }
 
 // ---------------------------------------------------------- shard format
-uint32_t crc32c(const uint8_t* p, size_t n) {
-  uint64_t c = 0xFFFFFFFFu;
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
+  uint64_t c = crc ^ 0xFFFFFFFFu;
   size_t i = 0;
   for (; i + 8 <= n; i += 8) {
     uint64_t v;
@@ -205,6 +205,13 @@ uint32_t crc32c(const uint8_t* p, size_t n) {
   return c32 ^ 0xFFFFFFFFu;
 }
 
+namespace {
+constexpr size_t kCrcAt = 124;
+uint32_t shard_crc(const uint8_t* wire, size_t S) {
+  return crc32c(wire + ShardHeader::kSize, S, crc32c(wire, kCrcAt));
+}
+}  // namespace
+
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   if (h.salt.size() > 32) throw Error("shard: salt longer than 32 bytes");
   Buffer w;
@@ -212,7 +219,7 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   w.resize(ShardHeader::kSize, 0);
   w.insert(w.end(), payload, payload + h.shard_size);
   std::memcpy(w.data(), "MECS", 4);
-  w[4] = h.version;
+  w[4] = ShardHeader::kVersion;
   w[5] = h.k;
   w[6] = h.m;
   w[7] = h.index;
@@ -222,8 +229,9 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   const uint32_t sl = (uint32_t)h.salt.size();
   std::memcpy(w.data() + 56, &sl, 4);
   if (sl) std::memcpy(w.data() + 60, h.salt.data(), sl);
-  const uint32_t crc = crc32c(w.data() + ShardHeader::kSize, h.shard_size);
-  std::memcpy(w.data() + 92, &crc, 4);
+  std::memcpy(w.data() + 92, h.owner.value.data(), 32);
+  const uint32_t crc = shard_crc(w.data(), h.shard_size);
+  std::memcpy(w.data() + kCrcAt, &crc, 4);
   return w;
 }
 
@@ -240,16 +248,16 @@ ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
   h.address = Address(w.data() + 24, 0, false);
   uint32_t sl;
   std::memcpy(&sl, w.data() + 56, 4);
+  if (h.version != ShardHeader::kVersion) throw ValidationFailed("shard: unknown version");
   if (sl > 32) throw ValidationFailed("shard: bad salt length");
   h.salt.assign(w.begin() + 60, w.begin() + 60 + sl);
-  std::memcpy(&h.crc, w.data() + 92, 4);
-  if (h.version != 1) throw ValidationFailed("shard: unknown version");
+  h.owner = Address(w.data() + 92, 0, false);
+  std::memcpy(&h.crc, w.data() + kCrcAt, 4);
   if (h.k < 1 || h.index >= h.k + h.m) throw ValidationFailed("shard: bad geometry");
   if (h.shard_size != memo_ec_shard_size(h.block_size, h.k))
     throw ValidationFailed("shard: size does not match block size");
   if (w.size() != ShardHeader::kSize + h.shard_size) throw ValidationFailed("shard: truncated");
-  if (crc32c(w.data() + ShardHeader::kSize, h.shard_size) != h.crc)
-    throw ValidationFailed("shard: checksum mismatch");
+  if (shard_crc(w.data(), h.shard_size) != h.crc) throw ValidationFailed("shard: checksum mismatch");
   if (payload) *payload = w.data() + ShardHeader::kSize;
   return h;
 }
@@ -337,6 +345,10 @@ void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
 }
 
 // --------------------------------------------------------------- plugin
+namespace {
+enum MemberEvent { kDiscovered = 0, kDisappeared = 1, kAppeared = 2 };
+}
+
 ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& overlay,
                                    ErasureOptions o)
     : StackedConsensus(std::move(backend)),
@@ -347,9 +359,26 @@ ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& 
   if (o_.k < 1 || o_.m < 1 || o_.k > MEMO_EC_MAX_K || o_.m > MEMO_EC_MAX_M)
     throw Error("erasure: bad (k, m)");
   bthread_ = std::thread([this] { batcher_loop(); });
+  if (o_.rescan) rescan();
+  mthread_ = std::thread([this] { membership_loop(); });
+  Overlay::Handlers h;
+  h.discovered = [this](const Address& id) { post(kDiscovered, id); };
+  h.disappeared = [this](const Address& id) { post(kDisappeared, id); };
+  h.appeared = [this](const Address& id) { post(kAppeared, id); };
+  sub_token_ = overlay_.subscribe(std::move(h));
+  // blocks the rescan found under-placed go to the nodes present now, as
+  // they would to a newcomer
+  if (o_.rescan && o_.auto_expand) post(kDiscovered, Address());
 }
 
 ErasureConsensus::~ErasureConsensus() {
+  overlay_.unsubscribe(sub_token_);
+  {
+    std::lock_guard<std::mutex> g(mmu_);
+    mstop_ = true;
+  }
+  mcv_.notify_all();
+  mthread_.join();
   {
     std::lock_guard<std::mutex> g(bmu_);
     bstop_ = true;
@@ -378,6 +407,8 @@ std::string ErasureConsensus::stats() const {
                   {"fetched", std::to_string(fetched_)},
                   {"decoded", std::to_string(decoded_)},
                   {"repaired", std::to_string(repaired_)},
+                  {"evictions", std::to_string(evictions_)},
+                  {"pending_evictions", std::to_string(pending_evictions())},
                   {"encode_calls", std::to_string(codec_.encode_calls())},
                   {"rebuild_calls", std::to_string(codec_.rebuild_calls())}});
 }
@@ -386,6 +417,58 @@ Buffer ErasureConsensus::padded(const Block& b, size_t S) const {
   Buffer p((size_t)o_.k * S, 0);
   std::copy(b.data.begin(), b.data.end(), p.begin());
   return p;
+}
+
+ShardHeader ErasureConsensus::header_of(const Address& a, const Placement& pl, int index) const {
+  ShardHeader h;
+  h.k = (uint8_t)o_.k;
+  h.m = (uint8_t)o_.m;
+  h.index = (uint8_t)index;
+  h.block_size = pl.B;
+  h.shard_size = memo_ec_shard_size(pl.B, o_.k);
+  h.address = a;
+  h.salt = pl.salt;
+  h.owner = pl.owner;
+  return h;
+}
+
+void ErasureConsensus::set_placement_locked(const Address& a, Placement pl) {
+  auto it = index_.find(a);
+  if (it != index_.end())
+    for (auto& h : it->second.holder) {
+      if (!h) continue;
+      auto nb = node_blocks_.find(h);
+      if (nb == node_blocks_.end()) continue;
+      nb->second.erase(a);
+      if (nb->second.empty()) node_blocks_.erase(nb);
+    }
+  for (auto& h : pl.holder)
+    if (h) node_blocks_[h].insert(a);
+  index_[a] = std::move(pl);
+}
+
+void ErasureConsensus::erase_placement_locked(const Address& a) {
+  auto it = index_.find(a);
+  if (it == index_.end()) return;
+  for (auto& h : it->second.holder) {
+    if (!h) continue;
+    auto nb = node_blocks_.find(h);
+    if (nb == node_blocks_.end()) continue;
+    nb->second.erase(a);
+    if (nb->second.empty()) node_blocks_.erase(nb);
+  }
+  index_.erase(it);
+}
+
+size_t ErasureConsensus::node_blocks(const Address& node) const {
+  std::shared_lock<std::shared_mutex> g(index_mu_);
+  auto it = node_blocks_.find(node);
+  return it == node_blocks_.end() ? 0 : it->second.size();
+}
+
+void ErasureConsensus::on_rebalanced(std::function<void(const Address&)> f) {
+  std::lock_guard<std::mutex> g(repair_mu_);
+  rebalanced_ = std::move(f);
 }
 
 // The batcher thread: gathers concurrent store() calls (up to batch_max
@@ -454,17 +537,11 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
   Placement pl;
   pl.B = b.data.size();
   pl.salt = b.salt;
-  pl.owner.assign(total, Address());
+  pl.owner = b.owner;
+  pl.holder.assign(total, Address());
   std::vector<int> ok(total, 0);
   auto put = [&](size_t i) {
-    ShardHeader h;
-    h.k = (uint8_t)o_.k;
-    h.m = (uint8_t)o_.m;
-    h.index = (uint8_t)i;
-    h.block_size = b.data.size();
-    h.shard_size = S;
-    h.address = b.address;
-    h.salt = b.salt;
+    const ShardHeader h = header_of(b.address, pl, (int)i);
     const uint8_t* p = i < (size_t)o_.k ? data + i * dstride : parity + (i - o_.k) * pstride;
     try {
       owners[i]->store(shard_key(b.address, (int)i), encode_shard(h, p));
@@ -478,12 +555,12 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
   int reached = 0;
   for (size_t i = 0; i < owners.size(); ++i)
     if (ok[i]) {
-      pl.owner[i] = owners[i]->id;
+      pl.holder[i] = owners[i]->id;
       ++reached;
     }
   {
     std::unique_lock<std::shared_mutex> g(index_mu_);
-    index_[b.address] = pl;
+    set_placement_locked(b.address, std::move(pl));
   }
   if (reached < o_.k)
     throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
@@ -493,7 +570,7 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
 
 void ErasureConsensus::_store(const Block& b, StoreMode mode) {
   if (b.is_mutable || b.address.mutable_block()) return backend_->store(b, mode);
-  if (!chb_valid(b.address, b.salt, b.data)) throw ValidationFailed("CHB address mismatch");
+  if (!chb_valid(b.address, b.salt, b.owner, b.data)) throw ValidationFailed("CHB address mismatch");
   EncodeJob job{&b, {}};
   auto fut = job.parity.get_future();
   {
@@ -520,7 +597,7 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
     std::vector<char> valid(n0, 0);
     pool_.parallel_for(n0, [&](size_t i) {
       const Block* b = imm[b0 + i];
-      valid[i] = chb_valid(b->address, b->salt, b->data);
+      valid[i] = chb_valid(b->address, b->salt, b->owner, b->data);
     });
     tm.lap("chb");
     std::map<int, std::vector<const Block*>> by_s;
@@ -554,11 +631,14 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
 }
 
 // Shards of block `a` until `want` distinct valid shards are in hand.
-// Invalid shards count as erasures.  First from the owners the placement
-// index records (Paxos::_node_blocks analogue): shard i from owner i, data
-// shards first.  Then, for blocks this client did not place or shards that
-// moved, from every node in lookup order, in waves.  parallel = false works
-// node by node (for callers already on the pool).
+// Invalid shards count as erasures, and so do shards of another block or
+// geometry: every accepted shard has the same header (but its index) as the
+// placement record, or, for a block this client did not place, as the first
+// shard accepted.  First from the owners the placement index records
+// (Paxos::_node_blocks analogue): shard i from owner i, data shards first.
+// Then, for blocks this client did not place or shards that moved, from
+// every node in lookup order, in waves.  parallel = false works node by
+// node (for callers already on the pool).
 std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
                                                                     bool& any_down,
                                                                     ShardHeader* hdr,
@@ -573,6 +653,8 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   };
   std::map<int, Buffer> got;
   std::mutex gm;
+  bool have_ref = false;
+  ShardHeader ref;
   any_down = false;
   auto have = [&](int i) {
     std::lock_guard<std::mutex> g(gm);
@@ -596,7 +678,12 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
       ShardHeader h = decode_shard(wire, nullptr);
       if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) return true;
       std::lock_guard<std::mutex> g(gm);
-      if (hdr && got.empty()) *hdr = h;
+      if (!have_ref) {
+        ref = h;
+        have_ref = true;
+      } else if (!h.same_block(ref)) {
+        return true;  // another geometry, salt or owner: an erasure
+      }
       got.emplace(i, std::move(wire));
     } catch (ValidationFailed&) {
       // corrupted shard: an erasure
@@ -609,21 +696,24 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
       for (size_t t = 0; t < n && count() < want; ++t) fn(t);
   };
 
-  std::vector<std::shared_ptr<Node>> owner(total);
+  std::vector<std::shared_ptr<Node>> holder(total);
   {
     std::shared_lock<std::shared_mutex> g(index_mu_);
     auto it = index_.find(a);
-    if (it != index_.end())
-      for (int i = 0; i < total && i < (int)it->second.owner.size(); ++i)
-        if (it->second.owner[i]) owner[i] = overlay_.node(it->second.owner[i]);
+    if (it != index_.end()) {
+      ref = header_of(a, it->second, 0);
+      have_ref = true;
+      for (int i = 0; i < total && i < (int)it->second.holder.size(); ++i)
+        if (it->second.holder[i]) holder[i] = overlay_.node(it->second.holder[i]);
+    }
   }
   for (int pass = 0; pass < 2 && count() < want; ++pass) {
     // pass 0: the data shards (no decode needed); pass 1: the parity shards
     key_upto(pass ? total : o_.k);
     std::vector<int> ids;
     for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i)
-      if (owner[i] && !owner[i]->evicted && !have(i)) ids.push_back(i);
-    run(ids.size(), [&](size_t t) { try_node(owner[ids[t]], ids[t]); });
+      if (holder[i] && !holder[i]->evicted && !have(i)) ids.push_back(i);
+    run(ids.size(), [&](size_t t) { try_node(holder[ids[t]], ids[t]); });
   }
 
   if (count() < want) {
@@ -640,6 +730,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
       next += wave;
     }
   }
+  if (hdr && have_ref) *hdr = ref;
   std::vector<std::pair<int, Buffer>> out;
   for (auto& kv : got) out.emplace_back(kv.first, std::move(kv.second));
   return out;
@@ -683,12 +774,13 @@ std::unique_ptr<Block> ErasureConsensus::assemble(const Address& a, Gathered& g,
   for (size_t r = 0; r < g.lost.size(); ++r)
     std::memcpy(block.data() + (size_t)g.lost[r] * S, rebuilt + r * stride, S);
   block.resize(g.h.block_size);
-  if (!chb_valid(a, g.h.salt, block))
+  if (!chb_valid(a, g.h.salt, g.h.owner, block))
     throw ValidationFailed("erasure: reassembled block does not match its address");
   auto b = std::make_unique<Block>();
   b->address = a;
   b->data = std::move(block);
   b->salt = g.h.salt;
+  b->owner = g.h.owner;
   ++fetched_;
   return b;
 }
@@ -793,6 +885,12 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
 
 void ErasureConsensus::_remove(const Address& a) {
   if (a.mutable_block()) return backend_->remove(a);
+  {
+    // forget the block first: a repair running concurrently will not
+    // re-place it (evict_removed_blocks, tests/doughnut.cc:1693-1719)
+    std::unique_lock<std::shared_mutex> g(index_mu_);
+    erase_placement_locked(a);
+  }
   for (auto& nd : overlay_.lookup(a, (int)overlay_.size()))
     for (int i = 0; i < o_.k + o_.m; ++i) {
       try {
@@ -800,133 +898,342 @@ void ErasureConsensus::_remove(const Address& a) {
       } catch (Error&) {
       }
     }
-  std::unique_lock<std::shared_mutex> g(index_mu_);
-  index_.erase(a);
 }
 
-ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
+// ------------------------------------------------------------- repair
+ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector<Address>& blocks,
+                                                               bool include_down) {
+  std::lock_guard<std::mutex> rl(repair_mu_);
   RepairReport rep;
+  rep.blocks_checked = blocks.size();
   const int k = o_.k, m = o_.m, total = k + m;
   struct Todo {
     Address a;
     Placement pl;
-    std::vector<int> lost, surv;
+    std::vector<int> lost;                       // shards to rebuild
+    std::vector<std::pair<int, Buffer>> surv;    // k validated survivor shards (wire)
+    bool skip = false;
   };
-  // scan every placed block's shards (on the pool; the index is copied
-  // first so the scan does not hold its lock)
-  std::vector<Todo> all;
-  {
-    std::shared_lock<std::shared_mutex> g(index_mu_);
-    all.reserve(index_.size());
-    for (auto& kv : index_) all.push_back(Todo{kv.first, kv.second, {}, {}});
-  }
-  rep.blocks_checked = all.size();
-  pool_.parallel_for(all.size(), [&](size_t b) {
-    Todo& t = all[b];
-    for (int i = 0; i < total; ++i) {
-      const Address& o = t.pl.owner[i];
-      auto nd = o ? overlay_.node(o) : nullptr;
-      bool ok = nd && !nd->evicted && (nd->up || !include_down);
-      if (ok && nd->up) ok = nd->has(shard_key(t.a, i));
-      if (ok) {
-        if (nd->up) t.surv.push_back(i);
-      } else {
-        t.lost.push_back(i);
+  // Chunks of blocks: the survivors of one chunk are held in memory at once.
+  const size_t chunk = (size_t)std::max(64, o_.batch_max) * std::max<size_t>(1, codec_.devices());
+  for (size_t c0 = 0; c0 < blocks.size(); c0 += chunk) {
+    const size_t cn = std::min(chunk, blocks.size() - c0);
+    std::vector<Todo> todo(cn);
+    // Scan: a shard is lost when its holder is gone (null, evicted, down
+    // with include_down), lacks it, or holds a copy that fails validation
+    // or belongs to another block or geometry; the first k valid shards
+    // found are the survivors.
+    pool_.parallel_for(cn, [&](size_t t) {
+      Todo& x = todo[t];
+      x.a = blocks[c0 + t];
+      {
+        std::shared_lock<std::shared_mutex> g(index_mu_);
+        auto it = index_.find(x.a);
+        if (it == index_.end()) {
+          x.skip = true;  // removed meanwhile
+          return;
+        }
+        x.pl = it->second;
       }
-    }
-  });
-  std::vector<Todo> todo;
-  for (auto& t : all) {
-    if (t.lost.empty()) continue;
-    if ((int)t.surv.size() < k) {
-      ++rep.unrecoverable;
-      continue;
-    }
-    todo.push_back(std::move(t));
-  }
-  // batches of blocks with the same (S, e): one GPU rebuild call each
-  std::map<std::pair<int, size_t>, std::vector<Todo*>> groups;
-  for (auto& t : todo) groups[{size_bucket(memo_ec_shard_size(t.pl.B, k)), t.lost.size()}].push_back(&t);
-  for (auto& g : groups) {
-    const int e = (int)g.first.second;
-    for (size_t b0 = 0; b0 < g.second.size(); b0 += o_.batch_max) {
-      const size_t n = std::min<size_t>(o_.batch_max, g.second.size() - b0);
-      size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
-      for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(g.second[b0 + bi]->pl.B, k));
-      std::vector<uint8_t> sidx(n * k), lidx(n * e);
-      Scratch surv(n * k * S), out(n * e * S);
-      std::vector<int> good(n, 1);
-      pool_.parallel_for(n, [&](size_t bi) {
-        Todo& t = *g.second[b0 + bi];
-        for (int s = 0; s < k; ++s) {
-          const int i = t.surv[s];
+      const ShardHeader ref = header_of(x.a, x.pl, 0);
+      for (int i = 0; i < total; ++i) {
+        const Address& o = i < (int)x.pl.holder.size() ? x.pl.holder[i] : Address();
+        auto nd = o ? overlay_.node(o) : nullptr;
+        if (!nd || nd->evicted || (!nd->up && include_down)) {
+          x.lost.push_back(i);
+          continue;
+        }
+        if (!nd->up) continue;  // unreachable for now: neither lost nor usable
+        const Key key = shard_key(x.a, i);
+        if ((int)x.surv.size() < k) {
+          Buffer w;
+          bool ok = false;
           try {
-            auto wire = overlay_.node(t.pl.owner[i])->fetch(shard_key(t.a, i));
-            const uint8_t* p = nullptr;
-            const ShardHeader h = decode_shard(wire, &p);
-            uint8_t* slot = surv.data() + (bi * k + s) * S;
-            std::memcpy(slot, p, h.shard_size);
-            std::memset(slot + h.shard_size, 0, S - h.shard_size);
-            sidx[bi * k + s] = (uint8_t)i;
-          } catch (Error&) {
-            good[bi] = 0;
-            return;
+            if (nd->try_fetch(key, w)) {
+              const ShardHeader h = decode_shard(w, nullptr);
+              ok = h.index == i && h.same_block(ref);
+            }
+          } catch (Unavailable&) {
+            continue;
+          } catch (ValidationFailed&) {
           }
+          if (ok) x.surv.emplace_back(i, std::move(w));
+          else x.lost.push_back(i);
+        } else if (!nd->has(key)) {
+          x.lost.push_back(i);
         }
-        for (int r = 0; r < e; ++r) lidx[bi * e + r] = (uint8_t)t.lost[r];
-      });
-      // survivors that failed validation: substitute nothing, retry next pass
-      for (size_t bi = 0; bi < n; ++bi)
-        if (!good[bi]) {
-          std::fill(sidx.begin() + bi * k, sidx.begin() + (bi + 1) * k, 0);
-          for (int s = 0; s < k; ++s) sidx[bi * k + s] = (uint8_t)s;
-        }
-      codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
-      ++rep.codec_calls;
-      pool_.parallel_for(n, [&](size_t bi) {
-        if (!good[bi]) return;
-        Todo& t = *g.second[b0 + bi];
-        std::set<Address> holders;
-        for (int i = 0; i < total; ++i)
-          if (t.pl.owner[i]) holders.insert(t.pl.owner[i]);
-        auto cand = overlay_.allocate(t.a, (int)overlay_.size());
-        size_t ci = 0;
-        for (int r = 0; r < e; ++r) {
-          const int i = t.lost[r];
-          ShardHeader h;
-          h.k = (uint8_t)k;
-          h.m = (uint8_t)m;
-          h.index = (uint8_t)i;
-          h.block_size = t.pl.B;
-          h.shard_size = memo_ec_shard_size(t.pl.B, k);
-          h.address = t.a;
-          h.salt = t.pl.salt;
-          const Buffer wire = encode_shard(h, out.data() + (bi * e + r) * S);
-          while (ci < cand.size()) {
-            auto& nd = cand[ci++];
-            if (holders.count(nd->id)) continue;
-            try {
-              nd->store(shard_key(t.a, i), wire);
-              t.pl.owner[i] = nd->id;
-              holders.insert(nd->id);
-              break;
-            } catch (Unavailable&) {
+      }
+    });
+    std::vector<Todo*> work;
+    for (auto& x : todo) {
+      if (x.skip || x.lost.empty()) continue;
+      if ((int)x.surv.size() < k) {
+        ++rep.unrecoverable;
+        continue;
+      }
+      work.push_back(&x);
+    }
+    // batches of blocks with the same (S bucket, e): one GPU rebuild call each
+    std::map<std::pair<int, size_t>, std::vector<Todo*>> groups;
+    for (auto* x : work) groups[{size_bucket(memo_ec_shard_size(x->pl.B, k)), x->lost.size()}].push_back(x);
+    for (auto& g : groups) {
+      const int e = (int)g.first.second;
+      for (size_t b0 = 0; b0 < g.second.size(); b0 += o_.batch_max) {
+        const size_t n = std::min<size_t>(o_.batch_max, g.second.size() - b0);
+        size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
+        for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(g.second[b0 + bi]->pl.B, k));
+        std::vector<uint8_t> sidx(n * k), lidx(n * e);
+        Scratch surv(n * k * S), out(n * e * S);
+        pool_.parallel_for(n, [&](size_t bi) {
+          Todo& x = *g.second[b0 + bi];
+          const size_t Sb = memo_ec_shard_size(x.pl.B, k);
+          for (int s = 0; s < k; ++s) {
+            uint8_t* slot = surv.data() + (bi * k + s) * S;
+            std::memcpy(slot, x.surv[s].second.data() + ShardHeader::kSize, Sb);
+            std::memset(slot + Sb, 0, S - Sb);
+            sidx[bi * k + s] = (uint8_t)x.surv[s].first;
+          }
+          for (int r = 0; r < e; ++r) lidx[bi * e + r] = (uint8_t)x.lost[r];
+          x.surv.clear();
+          x.surv.shrink_to_fit();
+        });
+        codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
+        ++rep.codec_calls;
+        std::vector<int> placed(n, 0);
+        // place each rebuilt shard on a reachable node holding none of the
+        // block's other shards (Overlay::allocate order); the stale copy on
+        // a reachable old holder is dropped
+        pool_.parallel_for(n, [&](size_t bi) {
+          Todo& x = *g.second[b0 + bi];
+          std::set<Address> taken;
+          for (int i = 0; i < total; ++i)
+            if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
+              taken.insert(x.pl.holder[i]);
+          auto cand = overlay_.allocate(x.a, (int)overlay_.size());
+          size_t ci = 0;
+          for (int r = 0; r < e; ++r) {
+            const int i = x.lost[r];
+            const Address old = x.pl.holder[i];
+            const Buffer wire = encode_shard(header_of(x.a, x.pl, i), out.data() + (bi * e + r) * S);
+            x.pl.holder[i] = Address();
+            while (ci < cand.size()) {
+              auto& nd = cand[ci++];
+              if (taken.count(nd->id)) continue;
+              try {
+                nd->store(shard_key(x.a, i), wire);
+                x.pl.holder[i] = nd->id;
+                taken.insert(nd->id);
+                ++placed[bi];
+                break;
+              } catch (Unavailable&) {
+              }
+            }
+            if (old && old != x.pl.holder[i]) {
+              auto on = overlay_.node(old);
+              if (on && on->up && !on->evicted) {
+                try {
+                  on->remove(shard_key(x.a, i));
+                } catch (Error&) {
+                }
+              }
             }
           }
+        });
+        for (size_t bi = 0; bi < n; ++bi) {
+          Todo& x = *g.second[b0 + bi];
+          bool removed = false;
+          {
+            std::unique_lock<std::shared_mutex> lk(index_mu_);
+            if (index_.count(x.a)) set_placement_locked(x.a, x.pl);
+            else removed = true;
+          }
+          if (removed) {  // removed while being repaired: drop the new shards
+            for (int i : x.lost)
+              if (x.pl.holder[i])
+                if (auto nd = overlay_.node(x.pl.holder[i])) {
+                  try {
+                    nd->remove(shard_key(x.a, i));
+                  } catch (Error&) {
+                  }
+                }
+            continue;
+          }
+          ++rep.blocks_repaired;
+          rep.shards_rebuilt += (size_t)placed[bi];
+          rep.shards_unplaced += (size_t)e - (size_t)placed[bi];
+          ++repaired_;
+          if (rebalanced_) rebalanced_(x.a);
         }
-      });
-      for (size_t bi = 0; bi < n; ++bi) {
-        if (!good[bi]) continue;
-        Todo& t = *g.second[b0 + bi];
-        std::unique_lock<std::shared_mutex> lk(index_mu_);
-        index_[t.a] = t.pl;
-        ++rep.blocks_repaired;
-        rep.shards_rebuilt += (size_t)e;
-        ++repaired_;
       }
     }
   }
   return rep;
+}
+
+ErasureConsensus::RepairReport ErasureConsensus::repair(bool include_down) {
+  std::vector<Address> all;
+  {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    all.reserve(index_.size());
+    for (auto& kv : index_) all.push_back(kv.first);
+  }
+  return repair_blocks(all, include_down);
+}
+
+ErasureConsensus::RepairReport ErasureConsensus::evict(const Address& node) {
+  if (auto nd = overlay_.node(node)) nd->evicted = true;  // lookup / allocate skip it
+  {
+    std::lock_guard<std::mutex> g(mmu_);
+    evict_at_.erase(node);
+  }
+  std::vector<Address> blocks;
+  {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    auto it = node_blocks_.find(node);
+    if (it != node_blocks_.end()) blocks.assign(it->second.begin(), it->second.end());
+  }
+  ++evictions_;
+  return repair_blocks(blocks, false);
+}
+
+ErasureConsensus::RepairReport ErasureConsensus::expand() {
+  std::vector<Address> under;
+  {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    for (auto& kv : index_)
+      for (auto& h : kv.second.holder)
+        if (!h) {
+          under.push_back(kv.first);
+          break;
+        }
+  }
+  return repair_blocks(under, false);
+}
+
+size_t ErasureConsensus::rescan() {
+  const int total = o_.k + o_.m;
+  struct Seen {
+    ShardHeader h;
+    Address node;
+  };
+  auto nodes = overlay_.nodes();
+  std::vector<std::vector<Seen>> per(nodes.size());
+  pool_.parallel_for(nodes.size(), [&](size_t ni) {
+    auto& nd = nodes[ni];
+    if (!nd->up || nd->evicted) return;
+    for (const Key& key : nd->silo->list()) {
+      Buffer w;
+      if (!nd->silo->try_get(key, w)) continue;
+      try {
+        ShardHeader h = decode_shard(w, nullptr);
+        // this code's shards only, under their own key
+        if (h.k != o_.k || h.m != o_.m || shard_key(h.address, h.index) != key) continue;
+        per[ni].push_back({std::move(h), nd->id});
+      } catch (ValidationFailed&) {
+        // not a shard (a mutable block's replica) or a damaged one
+      }
+    }
+  });
+  std::unordered_map<Address, Placement, AddressHash> found;
+  std::unordered_map<Address, ShardHeader, AddressHash> first;
+  for (auto& v : per)
+    for (auto& s : v) {
+      auto f = first.find(s.h.address);
+      if (f == first.end()) {
+        first.emplace(s.h.address, s.h);
+        Placement pl;
+        pl.B = s.h.block_size;
+        pl.salt = s.h.salt;
+        pl.owner = s.h.owner;
+        pl.holder.assign(total, Address());
+        f = first.find(s.h.address);
+        found.emplace(s.h.address, std::move(pl));
+      } else if (!s.h.same_block(f->second)) {
+        continue;  // disagrees with the block's first shard: not placed
+      }
+      Address& h = found[s.h.address].holder[s.h.index];
+      if (!h) h = s.node;
+    }
+  std::unique_lock<std::shared_mutex> g(index_mu_);
+  for (auto& kv : found) set_placement_locked(kv.first, std::move(kv.second));
+  return found.size();
+}
+
+// ---------------------------------------------------------- membership
+void ErasureConsensus::post(int kind, const Address& id) {
+  {
+    std::lock_guard<std::mutex> g(mmu_);
+    mq_.emplace_back(kind, id);
+  }
+  mcv_.notify_all();
+}
+
+size_t ErasureConsensus::pending_evictions() const {
+  std::lock_guard<std::mutex> g(mmu_);
+  return evict_at_.size();
+}
+
+// Membership thread (Paxos::LocalPeer's on_disappearance / on_discovery
+// handlers, Paxos.cc:730-745, 975-1009): a disappearance arms an eviction
+// timer that a return cancels; an expired timer evicts the node (its blocks'
+// shards rebuilt elsewhere); a discovery expands under-placed blocks.
+void ErasureConsensus::membership_loop() {
+  using clock = std::chrono::steady_clock;
+  std::unique_lock<std::mutex> l(mmu_);
+  while (!mstop_) {
+    if (mq_.empty()) {
+      if (evict_at_.empty()) {
+        mcv_.wait(l);
+      } else {
+        auto next = evict_at_.begin()->second;
+        for (auto& kv : evict_at_) next = std::min(next, kv.second);
+        if (clock::now() < next) mcv_.wait_until(l, next);
+      }
+      if (mstop_) break;
+    }
+    bool expand_now = false;
+    while (!mq_.empty()) {
+      const auto ev = mq_.front();
+      mq_.pop_front();
+      if (ev.first == kDisappeared) {
+        if (o_.eviction_delay_ms >= 0)
+          evict_at_[ev.second] = clock::now() + std::chrono::milliseconds(o_.eviction_delay_ms);
+      } else if (ev.first == kAppeared) {
+        evict_at_.erase(ev.second);
+      } else {
+        expand_now = expand_now || o_.auto_expand;
+      }
+    }
+    std::vector<Address> due;
+    const auto now = clock::now();
+    for (auto it = evict_at_.begin(); it != evict_at_.end();) {
+      if (it->second <= now) {
+        due.push_back(it->first);
+        it = evict_at_.erase(it);
+      } else {
+        ++it;
+      }
+    }
+    if (due.empty() && !expand_now) continue;
+    l.unlock();
+    for (auto& id : due) {
+      auto nd = overlay_.node(id);
+      if (!nd || nd->up) continue;  // came back
+      try {
+        evict(id);
+      } catch (std::exception& e) {
+        std::fprintf(stderr, "erasure: eviction of %s failed: %s\n", id.hex().c_str(), e.what());
+      }
+    }
+    if (expand_now) {
+      try {
+        expand();
+      } catch (std::exception& e) {
+        std::fprintf(stderr, "erasure: rebalancing failed: %s\n", e.what());
+      }
+    }
+    l.lock();
+  }
 }
 
 // "erasure" configuration: {"type": "erasure", "data-shards": k,
@@ -945,6 +1252,7 @@ struct RegisterErasure {
       o.m = get("parity-shards", 4);
       o.device = get("device", 0);
       o.batch_max = get("batch-max", 256);
+      o.eviction_delay_ms = (int64_t)get("eviction-delay", 600) * 1000;  // seconds
       const int f = get("backend-replication-factor", 3);
       return std::unique_ptr<Consensus>(
           new ErasureConsensus(std::make_unique<ReplicationConsensus>(ov, f), ov, o));

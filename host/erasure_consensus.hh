@@ -19,11 +19,13 @@
 // Mutable blocks stay on the backend (Paxos in memo, replication here).
 #pragma once
 
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
 #include <future>
 #include <thread>
+#include <unordered_set>
 
 #include "../include/memo_ec.h"
 #include "model.hh"
@@ -71,27 +73,38 @@ class Codec {
 };
 
 // ---------------------------------------------------------- shard format
-// On-wire / on-silo shard: a 96-byte header + S payload bytes.  The header
+// On-wire / on-silo shard: a 128-byte header + S payload bytes.  The header
 // replaces the CHB re-hash of LocalPeer::store (Paxos.cc:1571-1575) as the
-// per-shard validation (a shard is not a CHB).
-//   0 "MECS" | 4 version | 5 k | 6 m | 7 index | 8 u64 B | 16 u64 S |
-//   24 address[32] | 56 u32 salt_len | 60 salt[32] | 92 u32 crc32c(payload)
+// per-shard validation (a shard is not a CHB), and carries what the block's
+// own validation needs after reassembly (salt and owner, CHB.cc:264-289).
+//   0 "MECS" | 4 version (2) | 5 k | 6 m | 7 index | 8 u64 B | 16 u64 S |
+//   24 address[32] | 56 u32 salt_len | 60 salt[32] | 92 owner[32] |
+//   124 u32 crc32c(bytes 0..123 || payload)
+// The checksum covers the header too: a damaged size, salt or owner makes
+// the shard an erasure, not a poisoned reassembly.
 struct ShardHeader {
-  static constexpr size_t kSize = 96;
-  uint8_t version = 1;
+  static constexpr size_t kSize = 128;
+  static constexpr uint8_t kVersion = 2;
+  uint8_t version = kVersion;
   uint8_t k = 0, m = 0, index = 0;
   uint64_t block_size = 0, shard_size = 0;
   Address address;
   Buffer salt;
+  Address owner;  // the CHB owner (null: none)
   uint32_t crc = 0;
+  // Same block and code (every field but index and crc).
+  bool same_block(const ShardHeader& o) const {
+    return k == o.k && m == o.m && block_size == o.block_size && shard_size == o.shard_size &&
+           address == o.address && salt == o.salt && owner == o.owner;
+  }
 };
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
 // Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
-// payload length, CRC32C); throws ValidationFailed.
+// payload length, CRC32C over header and payload); throws ValidationFailed.
 ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
 // Silo key of shard `index` of block `address`.
 Key shard_key(const Address& address, int index);
-uint32_t crc32c(const uint8_t* p, size_t n);
+uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
 
 // ------------------------------------------------------------ thread pool
 // Parallel fan-out over peers (elle::reactor::for_each_parallel in memo).
@@ -118,6 +131,16 @@ struct ErasureOptions {
   int batch_max = 256;         // blocks per GPU encode / rebuild call
   int batch_window_us = 200;   // how long the batcher waits for company
   int threads = 16;            // peer fan-out (memo's background pool is <= 16)
+  // A node that disappears is evicted -- its shards rebuilt elsewhere --
+  // after this long unless it comes back ("eviction-delay", Paxos.cc:985-1009,
+  // default 10 min, Paxos.hxx:35).  < 0: never automatically.
+  int64_t eviction_delay_ms = 10 * 60 * 1000;
+  // Rebuild the placement index from the shard headers in the silos at
+  // start (LocalPeer::initialize's rebalancing inspector, Paxos.cc:747-784).
+  bool rescan = true;
+  // Rebuild under-placed blocks' missing shards onto newly discovered nodes
+  // (rebalance_auto_expand, Paxos.cc:1149-1244).
+  bool auto_expand = true;
 };
 
 class ErasureConsensus : public StackedConsensus {
@@ -130,13 +153,30 @@ class ErasureConsensus : public StackedConsensus {
 
   struct RepairReport {
     size_t blocks_checked = 0, blocks_repaired = 0, shards_rebuilt = 0;
-    size_t unrecoverable = 0, codec_calls = 0;
+    size_t unrecoverable = 0, codec_calls = 0, shards_unplaced = 0;
   };
-  // Rebuild every shard whose holder is evicted (or lost it), in batches of
-  // batch_max blocks per GPU call, and place it on a new owner.  With
-  // include_down, shards on nodes that are merely unreachable count as lost
-  // too (memo waits for the eviction delay, Paxos.cc:985-1009).
+  // Rebuild every shard whose holder is evicted, lacks it or holds an
+  // invalid copy, in batches of batch_max blocks per GPU call, and place it
+  // on a new owner.  With include_down, shards on nodes that are merely
+  // unreachable count as lost too.  A full scan of the index.
   RepairReport repair(bool include_down = false);
+  // Evict a node now (Paxos::LocalPeer::_disappeared_evict, Paxos.cc:1012-
+  // 1087): only the blocks the per-node index lists for it are repaired.
+  RepairReport evict(const Address& node);
+  // Place the missing shards of under-placed blocks (stored while fewer than
+  // k+m owners were reachable) on reachable nodes that hold none of the
+  // block's shards (the newcomer rebalancing of Paxos.cc:1149-1244).
+  RepairReport expand();
+  // Rebuild the placement and per-node indices from every reachable node's
+  // silo (shard headers); returns the number of blocks found.
+  size_t rescan();
+  // Called after a block's shards were rebuilt or re-placed (the reference's
+  // rebalanced() signal); runs on the repairing thread.
+  void on_rebalanced(std::function<void(const Address&)> f);
+  // Blocks the per-node index lists for `node` (Paxos.hh:403-434 by_node).
+  size_t node_blocks(const Address& node) const;
+  // Evictions scheduled and not yet run.
+  size_t pending_evictions() const;
   // Store many immutable blocks with one encode call per batch.
   void store_many(const std::vector<Block>& blocks);
   const Codec& codec() const { return codec_; }
@@ -152,7 +192,8 @@ class ErasureConsensus : public StackedConsensus {
   struct Placement {
     uint64_t B = 0;
     Buffer salt;
-    std::vector<Address> owner;  // holder of shard i (null: unplaced)
+    Address owner;                // CHB owner
+    std::vector<Address> holder;  // node holding shard i (null: unplaced)
   };
   struct EncodeJob {
     const Block* block;
@@ -171,6 +212,7 @@ class ErasureConsensus : public StackedConsensus {
   std::unique_ptr<Block> assemble(const Address& a, Gathered& g, const uint8_t* rebuilt,
                                   size_t stride);
   Buffer padded(const Block& b, size_t S) const;
+  ShardHeader header_of(const Address& a, const Placement& pl, int index) const;
   // parallel = false stores the shards one by one (callers on the pool).
   // Shard i of b to owner i: data shard j at data + j*dstride (nullptr: b's
   // own zero-padded payload), parity shard r at parity + r*pstride.
@@ -179,20 +221,40 @@ class ErasureConsensus : public StackedConsensus {
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);
+  // index_ and node_blocks_ together (callers hold index_mu_ exclusively)
+  void set_placement_locked(const Address& a, Placement pl);
+  void erase_placement_locked(const Address& a);
+  // The repair engine: rebuild and re-place the lost shards of `blocks`.
+  RepairReport repair_blocks(const std::vector<Address>& blocks, bool include_down);
+  // membership: overlay events -> the membership thread
+  void membership_loop();
+  void post(int kind, const Address& id);
 
   Overlay& overlay_;
   ErasureOptions o_;
   Codec codec_;
   ThreadPool pool_;
   mutable std::shared_mutex index_mu_;  // readers: fetch paths; writers: place, repair, remove
-  std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_node_blocks analogue
+  std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_quorums analogue
+  // node -> blocks it holds a shard of (Paxos::_node_blocks, Paxos.hh:403-434)
+  std::unordered_map<Address, std::unordered_set<Address, AddressHash>, AddressHash> node_blocks_;
+  std::mutex repair_mu_;  // one repair engine run at a time
+  std::function<void(const Address&)> rebalanced_;
   // batcher (host C++ batching of concurrent stores into one GPU call)
   std::mutex bmu_;
   std::condition_variable bcv_;
   std::deque<EncodeJob*> bq_;
   bool bstop_ = false;
   std::thread bthread_;
-  std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0};
+  // membership thread: discoveries, disappearances (eviction timers), returns
+  mutable std::mutex mmu_;
+  std::condition_variable mcv_;
+  std::deque<std::pair<int, Address>> mq_;
+  std::map<Address, std::chrono::steady_clock::time_point> evict_at_;
+  bool mstop_ = false;
+  int sub_token_ = -1;
+  std::thread mthread_;
+  std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0}, evictions_{0};
 };
 
 }  // namespace memo_host

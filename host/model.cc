@@ -59,12 +59,23 @@ std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b, size_t n
   return out;
 }
 
-Block make_chb(Buffer data, Buffer salt) {
+Address chb_address(const Buffer& data, const Address& owner, const Buffer& salt,
+                    const Version& version) {
+  // salt || owner (the owner only when set and version >= 0.4), then data
+  Buffer saltowner(salt);
+  if (owner && !(version < Version{0, 4, 0}))
+    saltowner.insert(saltowner.end(), owner.value.begin(), owner.value.end());
+  const auto h = sha256(saltowner.data(), saltowner.size(), data.data(), data.size());
+  return Address(h.data(), flags::immutable_block, !(version < Version{0, 5, 0}));
+}
+
+Block make_chb(Buffer data, Buffer salt, Address owner, const Version& version) {
   Block b;
-  const auto h = sha256(salt.data(), salt.size(), data.data(), data.size());
-  b.address = Address(h.data(), flags::immutable_block, true);
+  if (version < Version{0, 4, 0}) owner = Address();  // CHB.cc:44-46
+  b.address = chb_address(data, owner, salt, version);
   b.data = std::move(data);
   b.salt = std::move(salt);
+  b.owner = owner;
   return b;
 }
 
@@ -78,9 +89,10 @@ Block make_mutable(Address address, Buffer data, int version) {
   return b;
 }
 
-bool chb_valid(const Address& address, const Buffer& salt, const Buffer& data) {
-  const auto h = sha256(salt.data(), salt.size(), data.data(), data.size());
-  return Address(h.data(), flags::immutable_block, true) == address;
+bool chb_valid(const Address& address, const Buffer& salt, const Address& owner, const Buffer& data,
+               const Version& version) {
+  const Address want = chb_address(data, owner, salt, version);
+  return std::memcmp(want.value.data(), address.value.data(), 31) == 0;
 }
 
 // ---------------------------------------------------------------- silo
@@ -206,10 +218,35 @@ std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo>
   auto n = std::make_shared<Node>();
   n->id = id;
   n->silo = std::move(silo);
-  std::unique_lock<std::shared_mutex> g(mu_);
-  nodes_.push_back(n);
-  by_id_[n->id] = n;
+  {
+    std::unique_lock<std::shared_mutex> g(mu_);
+    nodes_.push_back(n);
+    by_id_[n->id] = n;
+  }
+  for (auto& h : handlers())
+    if (h.discovered) h.discovered(id);
   return n;
+}
+
+int Overlay::subscribe(Handlers h) {
+  std::lock_guard<std::mutex> g(hmu_);
+  handlers_[next_token_] = std::move(h);
+  return next_token_++;
+}
+
+void Overlay::unsubscribe(int token) {
+  std::lock_guard<std::mutex> g(hmu_);
+  handlers_.erase(token);
+}
+
+void Overlay::set_up(const Address& id, bool up) {
+  auto n = node(id);
+  if (!n) throw Error("overlay: unknown node " + id.hex());
+  if (n->up.exchange(up) == up) return;
+  for (auto& h : handlers()) {
+    const NodeEvent& f = up ? h.appeared : h.disappeared;
+    if (f) f(id);
+  }
 }
 
 std::shared_ptr<Node> Overlay::node(const Address& id) const {
@@ -294,28 +331,30 @@ namespace {
 Key replica_key(const Address& a) { return a; }
 
 Buffer encode_replica(const Block& b) {
-  // [version u32][salt len u32][salt][data]
-  Buffer out(8 + b.salt.size() + b.data.size());
+  // [version u32][salt len u32][owner 32][salt][data]
+  Buffer out(40 + b.salt.size() + b.data.size());
   const uint32_t v = (uint32_t)b.version, sl = (uint32_t)b.salt.size();
   std::memcpy(out.data(), &v, 4);
   std::memcpy(out.data() + 4, &sl, 4);
-  std::copy(b.salt.begin(), b.salt.end(), out.begin() + 8);
-  std::copy(b.data.begin(), b.data.end(), out.begin() + 8 + sl);
+  std::memcpy(out.data() + 8, b.owner.value.data(), 32);
+  std::copy(b.salt.begin(), b.salt.end(), out.begin() + 40);
+  std::copy(b.data.begin(), b.data.end(), out.begin() + 40 + sl);
   return out;
 }
 
 Block decode_replica(const Address& a, const Buffer& r) {
-  if (r.size() < 8) throw ValidationFailed("short replica");
+  if (r.size() < 40) throw ValidationFailed("short replica");
   uint32_t v, sl;
   std::memcpy(&v, r.data(), 4);
   std::memcpy(&sl, r.data() + 4, 4);
-  if (8 + (size_t)sl > r.size()) throw ValidationFailed("bad replica");
+  if (40 + (size_t)sl > r.size()) throw ValidationFailed("bad replica");
   Block b;
   b.address = a;
   b.version = (int)v;
   b.is_mutable = a.mutable_block();
-  b.salt.assign(r.begin() + 8, r.begin() + 8 + sl);
-  b.data.assign(r.begin() + 8 + sl, r.end());
+  b.owner = Address(r.data() + 8, 0, false);
+  b.salt.assign(r.begin() + 40, r.begin() + 40 + sl);
+  b.data.assign(r.begin() + 40 + sl, r.end());
   return b;
 }
 }  // namespace
@@ -346,7 +385,7 @@ std::unique_ptr<Block> ReplicationConsensus::_fetch(const Address& a) {
     try {
       auto r = o->fetch(replica_key(a));
       auto b = std::make_unique<Block>(decode_replica(a, r));
-      if (!b->is_mutable && !chb_valid(a, b->salt, b->data)) continue;
+      if (!b->is_mutable && !chb_valid(a, b->salt, b->owner, b->data)) continue;
       return b;
     } catch (Unavailable&) {
     } catch (silo::MissingKey&) {

@@ -96,22 +96,37 @@ struct AddressHash {
 std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b = nullptr, size_t nb = 0);
 
 // ----------------------------------------------------------------- blocks
+// The model version a network runs (Doughnut::version(), elle::Version
+// major.minor.patch).  CHB hashing depends on it (CHB.cc:270-289): the owner
+// enters the hash from 0.4.0, the immutable flag is combined into the
+// address from 0.5.0.
+using Version = std::array<int, 3>;
+constexpr Version kModelVersion{0, 9, 0};
+
 // blocks::Block (src/memo/model/blocks/Block.hh:107-200): an address and the
 // payload data() (Block.hh:142).  Immutable content-hash blocks are CHBs:
-// address = SHA-256(salt || data) with the immutable flag combined
-// (CHB::_hash_address, src/memo/model/doughnut/CHB.cc:264-289; owner = null).
+// address = SHA-256(salt || owner || data) (CHB::_hash_address,
+// src/memo/model/doughnut/CHB.cc:264-289), the owner only when set and the
+// version >= 0.4 (otherwise the block carries a null owner, CHB.cc:38-48).
 struct Block {
   Address address;
   Buffer data;
   Buffer salt;
+  Address owner;  // CHB owner (null: none); blocks::Block::owner()
   bool is_mutable = false;
   int version = 0;  // mutable blocks only
 };
 
-Block make_chb(Buffer data, Buffer salt = {});
+// CHB::_hash_address (CHB.cc:264-289).
+Address chb_address(const Buffer& data, const Address& owner, const Buffer& salt,
+                    const Version& version = kModelVersion);
+Block make_chb(Buffer data, Buffer salt = {}, Address owner = {},
+               const Version& version = kModelVersion);
 Block make_mutable(Address address, Buffer data, int version = 1);
-// CHB::validate (CHB.cc:79-99): the address is the hash of the content.
-bool chb_valid(const Address& address, const Buffer& salt, const Buffer& data);
+// CHB::_validate (CHB.cc:79-99): the address is the hash of the content,
+// compared without the flag byte (equal_unflagged, Address.cc:135-141).
+bool chb_valid(const Address& address, const Buffer& salt, const Address& owner,
+               const Buffer& data, const Version& version = kModelVersion);
 
 // ------------------------------------------------------------------- silo
 // silo::Silo (src/memo/silo/Silo.hh:33-129): get/set/erase/list with the
@@ -194,6 +209,20 @@ struct Node {
 // by rendezvous hashing of (address, node id), so every client agrees.
 class Overlay {
  public:
+  // Membership signals (overlay::Overlay::on_discovery / on_disappearance,
+  // src/memo/overlay/Overlay.hh:124-129; a node coming back is a discovery
+  // there, `appeared` here).  Handlers run on the thread that changed the
+  // membership and must not block.
+  using NodeEvent = std::function<void(const Address& id)>;
+  struct Handlers {
+    NodeEvent discovered, disappeared, appeared;
+  };
+  int subscribe(Handlers h);
+  void unsubscribe(int token);
+  // Node::up with the signal (a test may still flip Node::up silently).
+  void set_up(const Address& id, bool up);
+
+  // Adds the node and signals its discovery.
   std::shared_ptr<Node> add_node(const Address& id, std::unique_ptr<Silo> silo);
   std::shared_ptr<Node> node(const Address& id) const;
   // Every node in rendezvous order for `address` (reachable or not).
@@ -210,6 +239,15 @@ class Overlay {
   mutable std::shared_mutex mu_;
   std::vector<std::shared_ptr<Node>> nodes_;
   std::unordered_map<Address, std::shared_ptr<Node>, AddressHash> by_id_;
+  std::mutex hmu_;
+  std::map<int, Handlers> handlers_;
+  int next_token_ = 0;
+  std::vector<Handlers> handlers() {
+    std::lock_guard<std::mutex> g(hmu_);
+    std::vector<Handlers> out;
+    for (auto& kv : handlers_) out.push_back(kv.second);
+    return out;
+  }
 };
 
 // -------------------------------------------------------------- consensus

@@ -3,7 +3,9 @@
 // reference test it follows.  Tests tagged GPU run the codec (libmemo_ec on
 // an MI355X); the others need no GPU.
 //   usage: test_erasure [--cpu-only] [filter]
+#include <atomic>
 #include <chrono>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <random>
@@ -29,6 +31,16 @@ struct Reg {
   Reg(const char* n, bool g, void (*f)()) { tests().push_back({n, g, f}); }
 };
 int g_fail = 0;
+
+// Polls `pred` for up to `ms` milliseconds (background rebalancing).
+template <class F>
+bool wait_for(F pred, int ms = 20000) {
+  for (int t = 0; t < ms; t += 5) {
+    if (pred()) return true;
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  return pred();
+}
 
 #define TEST(name, gpu)                      \
   static void test_##name();                 \
@@ -72,17 +84,28 @@ struct Net {
   Overlay overlay;
   std::vector<std::shared_ptr<Node>> nodes;
   std::unique_ptr<ErasureConsensus> ec;
-  Net(int n, int k, int m, int batch_window_us = 200) {
-    for (int i = 0; i < n; ++i) {
-      uint8_t id[32] = {0};
-      id[0] = (uint8_t)(i + 1);
-      id[1] = 0x4d;
-      nodes.push_back(overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>()));
-    }
-    ErasureOptions o;
+  ErasureOptions o;
+  // eviction_delay_ms < 0: no automatic eviction (tests that drop nodes
+  // silently by Node::up are not disturbed)
+  Net(int n, int k, int m, int batch_window_us = 200, int64_t eviction_delay_ms = -1) {
+    for (int i = 0; i < n; ++i) add();
     o.k = k;
     o.m = m;
     o.batch_window_us = batch_window_us;
+    o.eviction_delay_ms = eviction_delay_ms;
+    restart();
+  }
+  std::shared_ptr<Node> add() {
+    uint8_t id[32] = {0};
+    id[0] = (uint8_t)(nodes.size() + 1);
+    id[1] = 0x4d;
+    nodes.push_back(overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>()));
+    return nodes.back();
+  }
+  // A fresh consensus over the same silos (a node restart): its index comes
+  // from the shard headers on disk.
+  void restart() {
+    ec.reset();
     ec = std::make_unique<ErasureConsensus>(std::make_unique<ReplicationConsensus>(overlay, 3),
                                             overlay, o);
   }
@@ -147,13 +170,15 @@ TEST(shard_format_round_trip_and_validation, false) {
   h.shard_size = memo_ec_shard_size(1000, 10);
   h.address = Address::random(flags::immutable_block);
   h.salt = bytes("salt");
+  h.owner = Address::random(flags::mutable_block);
   Buffer payload = random_bytes(h.shard_size, 7);
   Buffer w = encode_shard(h, payload.data());
   CHECK(w.size() == ShardHeader::kSize + h.shard_size);
   const uint8_t* p = nullptr;
   ShardHeader d = decode_shard(w, &p);
   CHECK(d.k == 10 && d.m == 4 && d.index == 12 && d.block_size == 1000);
-  CHECK(d.address == h.address && d.salt == h.salt);
+  CHECK(d.address == h.address && d.salt == h.salt && d.owner == h.owner);
+  CHECK(d.same_block(h));
   CHECK(std::memcmp(p, payload.data(), h.shard_size) == 0);
   Buffer bad = w;
   bad[ShardHeader::kSize + 5] ^= 1;  // payload bit flip
@@ -161,15 +186,25 @@ TEST(shard_format_round_trip_and_validation, false) {
   bad = w;
   bad[16] ^= 1;  // shard size inconsistent with block size
   CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  for (size_t at : {size_t(8), size_t(60), size_t(100), size_t(30)}) {  // B, salt, owner, address
+    bad = w;
+    bad[at] ^= 0x10;  // the checksum covers the header
+    CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  }
   bad = w;
   bad.resize(bad.size() - 1);
   CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
   bad = w;
   bad[0] = 'X';
   CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
-  // CRC32C known answer (RFC 3720 B.4: 32 bytes of zeros -> 0x8a9136aa)
+  bad = w;
+  bad[4] = 1;  // round-1 layout
+  CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
+  // CRC32C known answer (RFC 3720 B.4: 32 bytes of zeros -> 0x8a9136aa), and
+  // chaining: crc(a || b) = crc(b, crc(a))
   uint8_t z[32] = {0};
   CHECK(crc32c(z, 32) == 0x8a9136aau);
+  CHECK(crc32c(z + 13, 19, crc32c(z, 13)) == 0x8a9136aau);
 }
 
 TEST(config_registry, false) {
@@ -203,12 +238,38 @@ TEST(placement_is_deterministic_and_distinct, false) {
 TEST(chb_address_is_content_hash, false) {
   Block b = make_chb(bytes("\\_o<"), bytes("salt"));
   CHECK(!b.address.mutable_block());
-  CHECK(chb_valid(b.address, b.salt, b.data));
+  CHECK(chb_valid(b.address, b.salt, b.owner, b.data));
   Buffer other = b.data;
   other[0] ^= 1;
-  CHECK(!chb_valid(b.address, b.salt, other));
+  CHECK(!chb_valid(b.address, b.salt, b.owner, other));
 }
 
+// CHB::_hash_address (CHB.cc:264-289): SHA-256(salt || owner || data) when
+// the owner is set and the version >= 0.4; the flag byte is combined from
+// 0.5; validation ignores the flag byte (equal_unflagged).
+TEST(chb_owner_and_version, false) {
+  const Address owner = Address::random(flags::mutable_block);
+  const Buffer data = bytes("owned block"), salt = bytes("pepper");
+  Block b = make_chb(data, salt, owner);
+  CHECK(b.owner == owner);
+  Buffer so = salt;
+  so.insert(so.end(), owner.value.begin(), owner.value.end());
+  const auto h = sha256(so.data(), so.size(), data.data(), data.size());
+  CHECK(std::memcmp(b.address.value.data(), h.data(), 31) == 0);
+  CHECK(b.address.value[31] == flags::immutable_block);
+  CHECK(chb_valid(b.address, salt, owner, data));
+  CHECK(!chb_valid(b.address, salt, Address(), data));                       // owner dropped
+  CHECK(!chb_valid(b.address, salt, Address::random(flags::mutable_block), data));  // other owner
+  CHECK(make_chb(data, salt).address != b.address);
+  // before 0.4 the owner is ignored (and not kept); before 0.5 the flag byte
+  // is the hash's own
+  Block old = make_chb(data, salt, owner, Version{0, 3, 0});
+  CHECK(!old.owner);
+  CHECK(old.address == make_chb(data, salt, Address(), Version{0, 3, 0}).address);
+  const auto h0 = sha256(salt.data(), salt.size(), data.data(), data.size());
+  CHECK(old.address.value[31] == h0[31]);
+  CHECK(chb_valid(old.address, salt, owner, data, Version{0, 3, 0}));
+}
 // -------------------------------------------------------------- GPU tests
 // tests/doughnut.cc:320-335 (CHB): insert -> fetch equal -> remove.
 TEST(CHB, true) {
@@ -216,6 +277,7 @@ TEST(CHB, true) {
   Block b = make_chb(bytes("\\_o<"));
   net.ec->store(b);
   CHECK(net.holders(b.address, 14) == 14);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
   auto f = net.ec->fetch(b.address);
   CHECK(f->data == b.data);
   net.ec->remove(b.address);
@@ -457,6 +519,175 @@ TEST(multi_device_split_matches_single, true) {
     CHECK(std::memcmp(&o1[(b * 2) * S], &data[(b * k) * S], S) == 0);
     CHECK(std::memcmp(&o1[(b * 2 + 1) * S], &p1[(b * m + 2) * S], S) == 0);
   }
+}
+
+
+// An owned CHB (CHB.cc:264-289: the owner enters the address) stored as
+// shards and read back with 4 owners down: the shards carry the owner, the
+// reassembled block validates, and a shard set claiming another owner does
+// not pass for it.
+TEST(owned_chb_round_trip_degraded, true) {
+  Net net(16, 10, 4);
+  const Address owner = Address::random(flags::mutable_block);
+  Block b = make_chb(random_bytes(300001, 41), bytes("salt!"), owner);
+  net.ec->store(b);
+  auto owners = net.overlay.allocate(b.address, 14);
+  for (int i : {0, 2, 5, 13}) owners[i]->up = false;
+  auto f = net.ec->fetch(b.address);
+  CHECK(f->data == b.data && f->owner == owner && f->salt == b.salt);
+  CHECK(chb_valid(b.address, f->salt, f->owner, f->data));
+  // every reachable shard re-framed with another owner (a valid CRC): the
+  // fetch rejects them as another block's shards
+  const Address other = Address::random(flags::mutable_block);
+  for (auto& n : net.nodes)
+    for (int i = 0; i < 14; ++i) {
+      const Key key = shard_key(b.address, i);
+      if (!n->up || !n->has(key)) continue;
+      const uint8_t* p = nullptr;
+      ShardHeader h = decode_shard(n->silo->get(key), &p);
+      h.owner = other;
+      n->silo->set(key, encode_shard(h, p), false, true);
+    }
+  net.restart();  // no placement record: the first shard sets the reference
+  CHECK_THROW(net.ec->fetch(b.address), ValidationFailed);
+}
+
+// a survivor's header is checked against the placement
+// record before repair copies its payload.  A shard of another code planted
+// under a survivor's key (valid CRC, larger shard size) is an erasure: it is
+// rebuilt and replaced, not copied into the batch.
+TEST(repair_rejects_foreign_shard, true) {
+  Net net(20, 4, 2);
+  Block b = make_chb(random_bytes(40000, 5));
+  net.ec->store(b);
+  auto owners = net.overlay.allocate(b.address, 6);
+  // shard 1 replaced by a k = 2 shard of a 3x larger block, same address
+  ShardHeader h;
+  h.k = 2;
+  h.m = 1;
+  h.index = 1;
+  h.block_size = 120000;
+  h.shard_size = memo_ec_shard_size(120000, 2);
+  h.address = b.address;
+  Buffer junk = random_bytes(h.shard_size, 9);
+  owners[1]->silo->set(shard_key(b.address, 1), encode_shard(h, junk.data()), false, true);
+  owners[4]->evicted = true;
+  auto rep = net.ec->repair();
+  CHECK(rep.unrecoverable == 0 && rep.blocks_repaired == 1);
+  CHECK(rep.shards_rebuilt == 2);  // the evicted node's shard and the foreign one
+  for (int i = 0; i < 6; ++i) {
+    int valid = 0;
+    for (auto& n : net.nodes) {
+      Buffer w;
+      if (n->evicted || !n->silo->try_get(shard_key(b.address, i), w)) continue;
+      try {
+        ShardHeader x = decode_shard(w, nullptr);
+        valid += x.k == 4 && x.index == i;
+      } catch (ValidationFailed&) {
+      }
+    }
+    CHECK(valid == 1);
+  }
+  for (int i : {0, 2}) owners[i]->up = false;
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// tests/doughnut.cc:1514-1571 (expand_newcomer): a block stored while fewer
+// than k+m owners were reachable is under-placed; when new nodes join, its
+// missing shards are rebuilt onto them in the background.
+TEST(expand_newcomer, true) {
+  Net net(12, 10, 4);  // 12 nodes: shards 12 and 13 have no owner
+  std::vector<Address> rebalanced;
+  std::mutex mu;
+  net.ec->on_rebalanced([&](const Address& a) {
+    std::lock_guard<std::mutex> g(mu);
+    rebalanced.push_back(a);
+  });
+  Block b = make_chb(random_bytes(100000, 77));
+  net.ec->store(b);
+  CHECK(net.shards(b.address, 14) == 12);
+  net.add();
+  net.add();  // discovery -> rebalancing
+  CHECK(wait_for([&] { std::lock_guard<std::mutex> g(mu); return !rebalanced.empty(); }));
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK(net.holders(b.address, 14) == 14);
+  int down = 0;  // now m losses are survivable
+  for (auto& n : net.nodes)
+    if (down < 4 && net.ec->node_blocks(n->id)) {
+      n->up = false;
+      ++down;
+    }
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// tests/doughnut.cc:1609-1634 (expand_from_disk): a fresh consensus over the
+// same silos rebuilds its index from the shard headers; an under-placed
+// block found there is expanded onto the nodes present, and evicting a node
+// repairs exactly the blocks that node held (per-node index from disk).
+TEST(expand_from_disk, true) {
+  Net net(12, 10, 4);
+  std::vector<Block> blocks;
+  for (int i = 0; i < 24; ++i) blocks.push_back(make_chb(random_bytes(20000 + 777 * i, 300 + i)));
+  net.ec->store_many(blocks);
+  for (auto& b : blocks) CHECK(net.shards(b.address, 14) == 12);
+  net.ec.reset();        // the node goes away ...
+  net.add();
+  net.add();             // ... the network grows meanwhile ...
+  std::atomic<int> rebalanced{0};
+  net.o.rescan = true;
+  net.restart();         // ... and it restarts from its silos
+  net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
+  CHECK(wait_for([&] {
+    for (auto& b : blocks)
+      if (net.shards(b.address, 14) != 14) return false;
+    return true;
+  }));
+  // per-node index rebuilt: evict one holder, exactly its blocks repaired
+  std::shared_ptr<Node> victim;
+  for (auto& n : net.nodes)
+    if (!victim && net.ec->node_blocks(n->id) > 0) victim = n;
+  const size_t held = net.ec->node_blocks(victim->id);
+  CHECK(held > 0);
+  net.restart();  // the index once more from disk only
+  CHECK(net.ec->node_blocks(victim->id) == held);
+  victim->up = false;
+  auto rep = net.ec->evict(victim->id);
+  CHECK(rep.blocks_checked == held && rep.blocks_repaired == held && rep.unrecoverable == 0);
+  CHECK(net.ec->node_blocks(victim->id) == 0);
+  for (auto& b : blocks) CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// tests/doughnut.cc:1693-1719 (evict_removed_blocks) with the eviction timer
+// (Paxos.cc:985-1009): a node that disappears is evicted after the delay and
+// its blocks repaired, a removed block is not brought back; a node that
+// returns within the delay is not evicted.
+TEST(evict_removed_blocks, true) {
+  Net net(16, 10, 4, 200, /*eviction_delay_ms=*/150);
+  std::vector<Block> bs;
+  for (int i = 0; i < 3; ++i) bs.push_back(make_chb(random_bytes(50000, 900 + i)));
+  for (auto& b : bs) net.ec->store(b);
+  net.ec->remove(bs[1].address);
+  CHECK(net.shards(bs[1].address, 14) == 0);
+  std::shared_ptr<Node> a, c;
+  for (auto& n : net.nodes) {
+    if (!a && net.ec->node_blocks(n->id) == 2) a = n;
+    else if (!c && net.ec->node_blocks(n->id) >= 1) c = n;
+  }
+  CHECK(a && c);
+  // a blip shorter than the delay: no eviction
+  net.overlay.set_up(c->id, false);
+  CHECK(wait_for([&] { return net.ec->pending_evictions() == 1; }));
+  std::this_thread::sleep_for(std::chrono::milliseconds(30));
+  net.overlay.set_up(c->id, true);
+  // a real disappearance: evicted after ~150 ms, blocks repaired
+  net.overlay.set_up(a->id, false);
+  CHECK(wait_for([&] { return a->evicted.load() && net.ec->node_blocks(a->id) == 0; }));
+  CHECK(!c->evicted);
+  CHECK(net.ec->pending_evictions() == 0);
+  CHECK(net.shards(bs[0].address, 14) == 14 && net.shards(bs[2].address, 14) == 14);
+  CHECK(net.shards(bs[1].address, 14) == 0);
+  CHECK_THROW(net.ec->fetch(bs[1].address), MissingBlock);
+  for (int i : {0, 2}) CHECK(net.ec->fetch(bs[i].address)->data == bs[i].data);
 }
 
 // Redundancy JSON (Consensus::redundancy, Paxos.cc:2218-2225 shape).

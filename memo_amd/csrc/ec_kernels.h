@@ -68,6 +68,24 @@ constexpr int MAC_TAB_REGS = 2;
 constexpr int MAC_COEF_REGS = 6;
 // A tile = 256 16-byte columns = one workgroup of gf_mac_kernel.
 constexpr uint32_t MAC_TILE = 256;
+// Shard-index bytes per lane staged through registers by the fused rebuild
+// (the rest of a tile's indices, if any, are loaded after the shards).
+constexpr int DEC_IDX_REGS = 2;
+
+// What a MAC launch multiplies with: a precomputed table image (encode), a
+// per-block coefficient row from decode_coef_kernel (two-kernel rebuild), or
+// rows the tile derives from the shard indices itself (fused rebuild).
+enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2 };
+
+// LDS bytes of the fused rebuild's decode workspace for a tile of ns blocks:
+// GF log/antilog (1 KiB), LW0 (128 B), per block 3 survivor-mask words + a
+// fault word, the survivor and lost indices, log W_t and log Lam_l.
+// Per-wave LDS copy of the GF log/antilog tables + LW0 (wave-local decode).
+constexpr uint32_t DEC_WAVE_BYTES = 1152;
+__host__ __device__ constexpr uint32_t dec_r4(uint32_t x) { return (x + 3u) & ~3u; }
+__host__ __device__ constexpr uint32_t dec_ws_bytes(uint32_t ns, uint32_t k, uint32_t e) {
+  return 1024u + 128u + 16u * ns + 2u * dec_r4(ns * k) + 2u * dec_r4(ns * e);
+}
 
 // One (kin -> r) multiply-accumulate over n blocks.
 struct MacSeg {
@@ -92,6 +110,14 @@ struct MacSeg {
   uint32_t kin, r, kpad;
   uint32_t flat;          // 1: flattened (block, column) units; 0: tile inside one block
   uint32_t wg_begin;      // first workgroup of this segment
+  // fused rebuild (gf_rebuild_kernel): the tile derives its blocks' decode
+  // rows from the shard indices itself (coef unused)
+  const uint8_t* sidx;    // n x kin survivor indices (surv_idx order)
+  const uint8_t* lidx;    // n x r lost indices (lost_idx order)
+  const uint32_t* lw0;    // LW0(i) = log sigma(i) - log Pall(i), i < kin + m (bytes, per code)
+  uint32_t* status;       // set to 1 on an invalid survivor / lost index set
+  uint32_t m;             // parity shards of the code (kin + m = shard count)
+  uint32_t ws_dw;         // LDS dword offset of the decode workspace
 };
 
 struct MacLaunch {
@@ -138,8 +164,10 @@ int mac_rbound(int r);
 int mac_kchunk(int kin, int R);
 void table_image_host(const uint8_t* coef, uint32_t r, uint32_t kin, uint32_t R, uint32_t kpad,
                       uint32_t* out);
-hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                       hipStream_t st);
+// LW0 table of (k, m) for the fused rebuild: 128 bytes (entries i < k + m).
+void lw0_host(int k, int m, uint8_t* out);
 hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st);  // closed-form decode rows
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);
 hipError_t launch_sha256(const Sha256Args& a, hipStream_t st);

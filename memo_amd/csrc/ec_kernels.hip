@@ -502,12 +502,347 @@ __device__ __forceinline__ void stage_images(const MacSeg& sg, const Unit& u, ui
   }
 }
 
+// x mod 255 for x < 2^16 (sums of GF logs).
+__device__ __forceinline__ uint32_t mod255(uint32_t x) {
+  x = (x & 0xFFu) + (x >> 8);
+  x = (x & 0xFFu) + (x >> 8);
+  return x >= 255u ? x - 255u : x;
+}
+
+// ---- Fused rebuild: a tile derives its blocks' decode rows itself.
+// The closed form of decode_coef_kernel (below) per tile, in LDS, while the
+// tile's shard loads are in flight: the survivor and lost indices of the
+// tile's blocks (contiguous ranges of surv_idx / lost_idx) and the GF tables
+// are loaded ahead of the shard loads (vmcnt retires in order), then
+//   (a) indices, GF log/antilog and LW0 into LDS, survivor masks zeroed;
+//   (b) survivor bit set per block by LDS atomic OR (duplicates and
+//       out-of-range indices mark the block faulty);
+//   (c) log W_t per (block, survivor) and log Lam_l per (block, lost shard),
+//       each a sum over the block's m non-survivors (set bits of the mask
+//       complement);
+//   (d) the coefficients row_l[t] = W_t Lam_l / (l ^ s_t) of the tile's
+//       table slots, then their product-table images, as the two-kernel
+//       rebuild builds them from rows read back from HBM.
+// No decode rows travel through HBM and no second kernel runs: the step is
+// one launch (gf_rebuild_kernel).
+struct DecWs {
+  uint8_t* lg;     // log[256] exp[768] (the kGf image)
+  uint8_t* ex;
+  uint8_t* lw0;    // LW0(i), i < k + m
+  uint32_t* mask;  // per block: survivor bits 0..95 in 3 words, word 3 = fault
+  uint8_t* sv;     // ns x k survivor indices
+  uint8_t* lv;     // ns x e lost indices
+  uint8_t* lw;     // ns x k log W_t
+  uint8_t* llam;   // ns x e log Lam_l (mod 255), DEC_UNIT when l survived
+};
+constexpr uint32_t DEC_UNIT = 0xFFu;
+
+__device__ __forceinline__ DecWs dec_ws(uint32_t* base, uint32_t ns, uint32_t k, uint32_t e) {
+  DecWs w;
+  uint8_t* p = reinterpret_cast<uint8_t*>(base);
+  w.lg = p;
+  w.ex = p + 256;
+  w.lw0 = p + 1024;
+  w.mask = reinterpret_cast<uint32_t*>(p + 1152);
+  p += 1152 + 16 * ns;
+  w.sv = p;
+  p += dec_r4(ns * k);
+  w.lv = p;
+  p += dec_r4(ns * e);
+  w.lw = p;
+  p += dec_r4(ns * k);
+  w.llam = p;
+  return w;
+}
+
+// Registers staged ahead of the shard loads: index bytes z = tid + 256q of
+// the tile's [survivors ns*k | lost ns*e] range, one GF-table dword, one LW0
+// dword.
+struct DecRegs {
+  uint32_t v[DEC_IDX_REGS];
+  uint32_t gf, lw0;
+};
+__device__ __forceinline__ uint32_t dec_idx_byte(const MacSeg& sg, const Unit& u, uint32_t z,
+                                                 uint32_t nk) {
+  return z < nk ? sg.sidx[u.b_first * sg.kin + z] : sg.lidx[u.b_first * sg.r + (z - nk)];
+}
+__device__ __forceinline__ void dec_load(const MacSeg& sg, const Unit& u, DecRegs& x) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nk = u.nsets * sg.kin, total = nk + u.nsets * sg.r;
+#pragma unroll
+  for (int q = 0; q < DEC_IDX_REGS; ++q) {
+    const uint32_t z = tid + 256u * q;
+    x.v[q] = z < total ? dec_idx_byte(sg, u, z, nk) : 0u;
+  }
+  x.gf = reinterpret_cast<const uint32_t*>(&kGf)[tid];  // 256 dwords: log + exp
+  x.lw0 = tid < 32 ? sg.lw0[tid] : 0u;
+}
+
+__device__ __forceinline__ void dec_phase_a(const MacSeg& sg, const Unit& u, const DecWs& w,
+                                            const DecRegs& x) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t nk = u.nsets * sg.kin, total = nk + u.nsets * sg.r;
+  reinterpret_cast<uint32_t*>(w.lg)[tid] = x.gf;
+  if (tid < 32) reinterpret_cast<uint32_t*>(w.lw0)[tid] = x.lw0;
+  for (uint32_t t = tid; t < 4 * u.nsets; t += 256) w.mask[t] = 0u;
+#pragma unroll
+  for (int q = 0; q < DEC_IDX_REGS; ++q) {
+    const uint32_t z = tid + 256u * q;
+    if (z < total) (z < nk ? w.sv[z] : w.lv[z - nk]) = (uint8_t)x.v[q];
+  }
+  for (uint32_t z = tid + 256u * DEC_IDX_REGS; z < total; z += 256)
+    (z < nk ? w.sv[z] : w.lv[z - nk]) = (uint8_t)dec_idx_byte(sg, u, z, nk);
+}
+
+// (b) survivor masks; k is the compile-time chunk on the hot path.
+__device__ __forceinline__ void dec_phase_b(const Unit& u, const DecWs& w, uint32_t k,
+                                            uint32_t nt) {
+  for (uint32_t x = threadIdx.x; x < u.nsets * k; x += 256) {
+    const uint32_t set = x / k, s = w.sv[x];
+    uint32_t* mk = w.mask + 4 * set;
+    if (s >= nt) {
+      atomicOr(mk + 3, 1u);
+    } else {
+      const uint32_t bit = 1u << (s & 31);
+      if (atomicOr(mk + (s >> 5), bit) & bit) atomicOr(mk + 3, 1u);  // duplicate
+    }
+  }
+}
+
+// Sum of log(v ^ c) over the block's non-survivors c (set bits of the
+// complement of its mask inside [0, nt)): m lookups for a valid block.
+__device__ __forceinline__ uint32_t dec_comp_sum(const DecWs& w, const uint32_t* mk, uint32_t v,
+                                                 uint32_t nt) {
+  uint32_t acc = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < 3; ++q) {
+    const uint32_t lo = 32u * q;
+    uint32_t valid = nt <= lo ? 0u : (nt - lo >= 32u ? ~0u : (1u << (nt - lo)) - 1u);
+    uint32_t c = ~mk[q] & valid;
+    while (c) {
+      const uint32_t b = __builtin_ctz(c);
+      c &= c - 1;
+      acc += w.lg[v ^ (lo + b)];
+    }
+  }
+  return acc;
+}
+
+// (c) log W_t per survivor slot, log Lam_l per lost slot.
+template <int R>
+__device__ __forceinline__ void dec_phase_c(const Unit& u, const DecWs& w, uint32_t k, uint32_t e,
+                                            uint32_t nt) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t x = tid; x < u.nsets * k; x += 256) {
+    const uint32_t set = x / k;
+    const uint32_t* mk = w.mask + 4 * set;
+    if (mk[3]) continue;  // faulty block: its coefficients are zero
+    const uint32_t s = w.sv[x];
+    w.lw[x] = (uint8_t)mod255(w.lw0[s] + dec_comp_sum(w, mk, s, nt));
+  }
+  for (uint32_t y = tid; y < u.nsets * R; y += 256) {
+    const uint32_t set = y / R, i = y - set * R;
+    if (i >= e) continue;
+    uint32_t* mk = w.mask + 4 * set;
+    const uint32_t l = w.lv[set * e + i];
+    if (l >= nt) {
+      atomicOr(mk + 3, 1u);
+      continue;
+    }
+    const bool surv = (mk[l >> 5] >> (l & 31)) & 1u;
+    // log Lam_l = -(LW0(l) + sum_c log(l ^ c)); c == l adds log[0] = 0
+    w.llam[set * e + i] =
+        (uint8_t)(surv ? DEC_UNIT : mod255(255u - mod255(w.lw0[l] + dec_comp_sum(w, mk, l, nt))));
+  }
+}
+
+// (d) coefficient of table slot ci = (set, row i, column j), kp columns per
+// row, R rows per set.  Faulty blocks report through the status word.
+template <int R>
+__device__ __forceinline__ uint32_t dec_coef(const Unit& u, const DecWs& w, uint32_t ci,
+                                             uint32_t kp, uint32_t k, uint32_t e) {
+  const uint32_t per = R * kp;
+  const uint32_t set = ci / per, rem = ci - set * per;
+  const uint32_t i = rem / kp, j = rem - i * kp;
+  if (set >= u.nsets || i >= e || j >= k || w.mask[4 * set + 3]) return 0u;
+  const uint32_t l = w.lv[set * e + i], s = w.sv[set * k + j], ll = w.llam[set * e + i];
+  if (ll == DEC_UNIT) return s == l ? 1u : 0u;
+  return w.ex[w.lw[set * k + j] + ll + 255u - w.lg[l ^ s]];  // < 765
+}
+__device__ __forceinline__ void dec_report(const MacSeg& sg, const Unit& u, const DecWs& w) {
+  for (uint32_t set = threadIdx.x; set < u.nsets; set += 256)
+    if (w.mask[4 * set + 3] && sg.status) *sg.status = 1u;  // plain store: every writer stores 1
+}
+
+// ---- Fused rebuild, hot path (kin == KC): wave-local decode.
+// Each of the tile's blocks is decoded by a group of L lanes (L = the power
+// of two >= KC) inside one wave, so no workgroup barrier separates the
+// decode steps: lane t holds survivor s_t and lost index l_t; the block's
+// survivor bit set is OR-reduced across the group with __shfl_xor; lane t
+// forms log W_t and log Lam_{l_t} from the m non-survivors; the l_r and
+// log Lam_r are broadcast in the group, and lane t builds column t of the
+// block's R product-table rows straight into the tile's LDS tables.  Each
+// wave has its own copy of the GF log/antilog tables and LW0 (1152 bytes),
+// so the tile's only barrier is the one before the MAC, as in encode.
+template <int KC>
+constexpr int dec_lanes() {
+  return KC <= 4 ? 4 : KC <= 8 ? 8 : 16;
+}
+template <int KC, int R>
+constexpr bool dec_wave_ok() {
+  return R <= dec_lanes<KC>();  // lost index r lives in lane r of the group
+}
+// The first DEC_PASSES passes (sets g, g + G) have their indices loaded
+// ahead of the shard loads; later passes (tiles of > 2G blocks) load theirs
+// when they run.
+constexpr int DEC_PASSES = 2;
+
+struct DecWaveRegs {
+  uint32_t sv[DEC_PASSES], lv[DEC_PASSES];
+  uint32_t gf[4], lw0;
+};
+
+template <int KC>
+__device__ __forceinline__ void dec_wave_idx(const MacSeg& sg, const Unit& u, uint32_t set,
+                                             uint32_t t, uint32_t& sv, uint32_t& lv) {
+  const bool live = set < u.nsets;
+  const uint64_t b = u.b_first + set;
+  sv = (live && t < (uint32_t)KC) ? sg.sidx[b * KC + t] : 0u;
+  lv = (live && t < sg.r) ? sg.lidx[b * sg.r + t] : 0u;
+}
+
+template <int KC>
+__device__ __forceinline__ void dec_wave_load(const MacSeg& sg, const Unit& u, DecWaveRegs& x) {
+  constexpr uint32_t L = dec_lanes<KC>(), G = 256 / L;
+  const uint32_t tid = threadIdx.x, t = tid % L, g = tid / L;
+#pragma unroll
+  for (int p = 0; p < DEC_PASSES; ++p) dec_wave_idx<KC>(sg, u, g + G * p, t, x.sv[p], x.lv[p]);
+  const uint32_t lane = tid % 64;
+  const uint32_t* gf = reinterpret_cast<const uint32_t*>(&kGf);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) x.gf[q] = gf[lane + 64 * q];
+  x.lw0 = lane < 32 ? sg.lw0[lane] : 0u;
+}
+
+// One block (set) decoded by its L-lane group; column t of its rows built
+// into the set's table images.  sv / lv: this lane's survivor / lost index.
+template <int KC, int R>
+__device__ __forceinline__ void dec_wave_set(const MacSeg& sg, const Unit& u, uint32_t set,
+                                             uint32_t sv, uint32_t lv, const uint8_t* lg,
+                                             const uint8_t* ex, const uint8_t* lw0,
+                                             uint32_t* s_tab) {
+  constexpr uint32_t L = dec_lanes<KC>();
+  const uint32_t t = threadIdx.x % L;
+  const uint32_t nt = KC + sg.m, e = sg.r;
+  const bool col = t < (uint32_t)KC, lost = t < e;
+  // survivor bit set (3 words: nt <= 80) and the faults, over the group
+  bool bad = (col && sv >= nt) || (lost && lv >= nt);
+  uint32_t mk0 = 0, mk1 = 0, mk2 = 0;
+  if (col && sv < nt) {
+    const uint32_t w = sv >> 5, bit = 1u << (sv & 31);
+    mk0 = w == 0 ? bit : 0u;
+    mk1 = w == 1 ? bit : 0u;
+    mk2 = w == 2 ? bit : 0u;
+  }
+  uint32_t badw = bad ? 1u : 0u;
+#pragma unroll
+  for (uint32_t off = 1; off < L; off <<= 1) {
+    mk0 |= __shfl_xor(mk0, off, L);
+    mk1 |= __shfl_xor(mk1, off, L);
+    mk2 |= __shfl_xor(mk2, off, L);
+    badw |= __shfl_xor(badw, off, L);
+  }
+  // out of range anywhere, or duplicate survivors (fewer than k distinct)
+  bad = badw != 0 || (uint32_t)(__popc(mk0) + __popc(mk1) + __popc(mk2)) != (uint32_t)KC;
+  const uint32_t mk[3] = {mk0, mk1, mk2};
+  auto comp_sum = [&](uint32_t v) {  // sum of log(v ^ c) over the non-survivors c
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      const uint32_t lo = 32u * q;
+      const uint32_t valid = nt <= lo ? 0u : (nt - lo >= 32u ? ~0u : (1u << (nt - lo)) - 1u);
+      uint32_t c = ~mk[q] & valid;
+      while (c) {
+        const uint32_t b = __builtin_ctz(c);
+        c &= c - 1;
+        acc += lg[v ^ (lo + b)];
+      }
+    }
+    return acc;
+  };
+  uint32_t lw = 0, llam = 0;  // log W_t; log Lam_{l_t} (DEC_UNIT: l_t survived)
+  if (!bad) {
+    if (col) lw = mod255(lw0[sv] + comp_sum(sv));
+    if (lost) {
+      const bool surv = (mk[lv >> 5] >> (lv & 31)) & 1u;
+      llam = surv ? DEC_UNIT : mod255(255u - mod255(lw0[lv] + comp_sum(lv)));
+    }
+  }
+  // coefficients row_r[t] for r < e (rows >= e and columns >= k are zero)
+  uint32_t cf[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const uint32_t l = __shfl(lv, r, L), ll = __shfl(llam, r, L);
+    uint32_t c = 0;
+    if (!bad && col && (uint32_t)r < e)
+      c = ll == DEC_UNIT ? (sv == l ? 1u : 0u) : ex[lw + ll + 255u - lg[l ^ sv]];  // < 765
+    cf[r] = c;
+  }
+  if (bad && t == 0 && sg.status) *sg.status = 1u;  // plain store: every writer stores 1
+  if (!col) return;  // lanes past KC: no column (kpad == KC on the hot path)
+  constexpr uint32_t per = R * KC;
+  const uint32_t base = set * per + t;  // slot of (set, row 0, column t)
+#pragma unroll
+  for (int r0 = 0; r0 < R; r0 += 4) {
+    uint4 q[4];
+    uint32_t lo[4];
+    coef_image4(pack4(cf[r0], r0 + 1 < R ? cf[r0 + 1] : 0u, r0 + 2 < R ? cf[r0 + 2] : 0u,
+                      r0 + 3 < R ? cf[r0 + 3] : 0u),
+                q, lo);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      if (r0 + a < R) put_image(s_tab, sg, per, base + (uint32_t)(r0 + a) * KC, q[a], lo[a]);
+  }
+}
+
+template <int KC, int R>
+__device__ __forceinline__ void dec_wave_tile(const MacSeg& sg, const Unit& u, const DecWaveRegs& x,
+                                              uint32_t* s_tab) {
+  constexpr uint32_t L = dec_lanes<KC>(), G = 256 / L;
+  const uint32_t tid = threadIdx.x, t = tid % L, g = tid / L, lane = tid % 64;
+  // this wave's GF tables + LW0 (written and read by this wave only: LDS
+  // operations of one wave complete in order)
+  uint32_t* wv = s_tab + sg.ws_dw + (tid / 64) * (DEC_WAVE_BYTES / 4);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) wv[lane + 64 * q] = x.gf[q];
+  if (lane < 32) wv[256 + lane] = x.lw0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(wv);
+  const uint8_t* ex = lg + 256;
+  const uint8_t* lw0 = lg + 1024;
+#pragma unroll
+  for (int p = 0; p < DEC_PASSES; ++p) {
+    const uint32_t set = g + G * p;
+    if (set < u.nsets) dec_wave_set<KC, R>(sg, u, set, x.sv[p], x.lv[p], lg, ex, lw0, s_tab);
+  }
+  for (uint32_t set = g + G * DEC_PASSES; set < u.nsets; set += G) {
+    uint32_t sv, lv;
+    dec_wave_idx<KC>(sg, u, set, t, sv, lv);
+    dec_wave_set<KC, R>(sg, u, set, sv, lv, lg, ex, lw0, s_tab);
+  }
+}
+
 // One tile of segment sg: KC is the straight-line shard chunk (kin == KC is
-// the hot path; other kin loop over chunks of KC shards).  COEF: the tables
-// are built from per-block coefficient rows (rebuild), else copied from a
-// precomputed image (encode).
-template <int KC, int R, bool NT, bool COEF>
+// the hot path; other kin loop over chunks of KC shards).  MODE: the tables
+// are copied from a precomputed image (MAC_ENCODE), built from per-block
+// coefficient rows in HBM (MAC_ROWS) or from rows the tile decodes itself
+// (MAC_FUSED).
+template <int KC, int R, bool NT, int MODE>
 __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32_t* s_tab) {
+  constexpr bool COEF = MODE != MAC_ENCODE;  // tables built in LDS from coefficients
+  constexpr bool FUSED = MODE == MAC_FUSED;
   const uint32_t kin = sg.kin, kpad = sg.kpad;
   const uint32_t set_dw = R * kpad * 8;
 
@@ -529,7 +864,69 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
 #pragma unroll
     for (int w = 0; w < 4; ++w) acc[i][w] = 0;
 
-  if (kin == KC) {
+  if constexpr (FUSED) {
+    const uint32_t nt = kin + sg.m, e = sg.r;
+    if (kin == KC && dec_wave_ok<KC, R>()) {
+      // hot path: wave-local decode, one barrier (before the MAC)
+      DecWaveRegs xw;
+      dec_wave_load<KC>(sg, u, xw);  // ahead of the shard loads
+      uint4 d[KC];
+#pragma unroll
+      for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
+      dec_wave_tile<KC, R>(sg, u, xw, s_tab);
+      __syncthreads();
+      mac_chunk<KC, R>(acc, d, tab, kpad, 0);
+    } else if (kin == KC) {
+      const DecWs ws = dec_ws(s_tab + sg.ws_dw, u.nsets, kin, e);
+      DecRegs xr;
+      dec_load(sg, u, xr);  // ahead of the shard loads
+      uint4 d[KC];
+#pragma unroll
+      for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
+      dec_phase_a(sg, u, ws, xr);
+      __syncthreads();
+      dec_phase_b(u, ws, KC, nt);
+      __syncthreads();
+      dec_phase_c<R>(u, ws, KC, e, nt);
+      __syncthreads();
+      uint32_t cv[MAC_COEF_REGS];
+#pragma unroll
+      for (int q = 0; q < MAC_COEF_REGS; ++q)
+        cv[q] = dec_coef<R>(u, ws, threadIdx.x + 256u * q, KC, KC, e);
+      dec_report(sg, u, ws);
+      store_images<R, KC>(sg, u, cv, s_tab);
+      __syncthreads();
+      mac_chunk<KC, R>(acc, d, tab, kpad, 0);
+    } else {
+      const DecWs ws = dec_ws(s_tab + sg.ws_dw, u.nsets, kin, e);
+      DecRegs xr;
+      dec_load(sg, u, xr);
+      dec_phase_a(sg, u, ws, xr);
+      __syncthreads();
+      dec_phase_b(u, ws, kin, nt);
+      __syncthreads();
+      dec_phase_c<R>(u, ws, kin, e, nt);
+      __syncthreads();
+      {
+        const uint32_t per = R * kpad, total = u.nsets * per;
+        for (uint32_t ci = threadIdx.x; ci < total; ci += 256) {
+          uint4 q;
+          uint32_t lo;
+          coef_image(dec_coef<R>(u, ws, ci, kpad, kin, e), q, lo);
+          put_image(s_tab, sg, per, ci, q, lo);
+        }
+      }
+      dec_report(sg, u, ws);
+      __syncthreads();
+      for (uint32_t j0 = 0; j0 < kin; j0 += KC) {
+        uint4 d[KC];
+#pragma unroll
+        for (int g = 0; g < KC; ++g)
+          if (j0 + g < kin) d[g] = ld16<NT>(u.pin + (uint64_t)(j0 + g) * sg.in_sstride);
+        mac_chunk<KC, R>(acc, d, tab, kpad, j0);
+      }
+    }
+  } else if (kin == KC) {
     // Hot path.  The table image loads go out first (vmcnt retires in issue
     // order, so the LDS copy then waits only for them), the KC shard loads
     // right behind; the barrier and table copy overlap the shard loads.
@@ -595,6 +992,7 @@ constexpr int mac_min_waves() {
   return (KC == 16 && R <= 4) ? MEMO_EC_MAC_W16 : 1;
 }
 
+// Encode (MAC_ENCODE) and the two-kernel rebuild's MAC (MAC_ROWS).
 template <int KC, int R, bool NT, bool COEF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(mac_min_waves<KC, R>())))
 gf_mac_kernel(const MacLaunch L) {
@@ -602,7 +1000,18 @@ gf_mac_kernel(const MacLaunch L) {
   uint32_t sid;
   uint64_t tile;
   if (!seg_tile(L, sid, tile)) return;
-  mac_tile<KC, R, NT, COEF>(L.seg[sid], tile, s_tab);
+  mac_tile<KC, R, NT, COEF ? MAC_ROWS : MAC_ENCODE>(L.seg[sid], tile, s_tab);
+}
+
+// Rebuild in one launch: decode rows derived per tile, then the MAC.
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(mac_min_waves<KC, R>())))
+gf_rebuild_kernel(const MacLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
+  uint32_t sid;
+  uint64_t tile;
+  if (!seg_tile(L, sid, tile)) return;
+  mac_tile<KC, R, NT, MAC_FUSED>(L.seg[sid], tile, s_tab);
 }
 
 // ------------------------------------------------- closed-form decode rows
@@ -626,11 +1035,6 @@ gf_mac_kernel(const MacLaunch L) {
 // elimination (round 1's decode_rows_reg_kernel: DESIGN.md 4.2).  Checked
 // against the oracle's
 // Gauss-Jordan rows (tests/test_gpu_parity.py).
-__device__ __forceinline__ uint32_t mod255(uint32_t x) {
-  x = (x & 0xFFu) + (x >> 8);
-  x = (x & 0xFFu) + (x >> 8);
-  return x >= 255u ? x - 255u : x;
-}
 
 // LW0(i) = log sigma(i) - log Pall(i) for i < k + m, into LDS.
 __device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_t nt,
@@ -1079,9 +1483,11 @@ hipError_t launch_sha256(const Sha256Args& a, hipStream_t st) {
 
 // ------------------------------------------------------------- launchers
 template <int KC, int R>
-static hipError_t launch_mac_t(bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+static hipError_t launch_mac_t(int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                                hipStream_t st) {
-  if (coef)
+  if (mode == MAC_FUSED)
+    hipLaunchKernelGGL((gf_rebuild_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
+  else if (mode == MAC_ROWS)
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, true>), dim3(grid), dim3(256), lds, st, L);
   else
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, false>), dim3(grid), dim3(256), lds, st, L);
@@ -1089,11 +1495,11 @@ static hipError_t launch_mac_t(bool coef, const MacLaunch& L, uint32_t grid, siz
 }
 
 template <int KC>
-static hipError_t launch_mac_r(int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+static hipError_t launch_mac_r(int R, int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                                hipStream_t st) {
   switch (R) {
 #define MEMO_EC_R(x) \
-  case x: return launch_mac_t<KC, x>(coef, L, grid, lds, st);
+  case x: return launch_mac_t<KC, x>(mode, L, grid, lds, st);
     MEMO_EC_R(1) MEMO_EC_R(2) MEMO_EC_R(3) MEMO_EC_R(4) MEMO_EC_R(6) MEMO_EC_R(8)
     MEMO_EC_R(12) MEMO_EC_R(16)
 #undef MEMO_EC_R
@@ -1122,30 +1528,30 @@ int mac_kchunk(int kin, int R) {
 // Shard chunks instantiated only for R <= 4 (common codes: RS(6,3),
 // RS(12,4), RS(14,4)); larger R takes the 4-shard chunk loop.
 template <int KC>
-static hipError_t launch_mac_r4(int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+static hipError_t launch_mac_r4(int R, int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                                 hipStream_t st) {
   switch (R) {
-    case 1: return launch_mac_t<KC, 1>(coef, L, grid, lds, st);
-    case 2: return launch_mac_t<KC, 2>(coef, L, grid, lds, st);
-    case 3: return launch_mac_t<KC, 3>(coef, L, grid, lds, st);
-    case 4: return launch_mac_t<KC, 4>(coef, L, grid, lds, st);
+    case 1: return launch_mac_t<KC, 1>(mode, L, grid, lds, st);
+    case 2: return launch_mac_t<KC, 2>(mode, L, grid, lds, st);
+    case 3: return launch_mac_t<KC, 3>(mode, L, grid, lds, st);
+    case 4: return launch_mac_t<KC, 4>(mode, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
 }
 
-hipError_t launch_mac(int KC, int R, bool coef, const MacLaunch& L, uint32_t grid, size_t lds,
+hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                       hipStream_t st) {
   switch (KC) {
-    case 2: return launch_mac_r<2>(R, coef, L, grid, lds, st);
-    case 3: return launch_mac_r<3>(R, coef, L, grid, lds, st);
-    case 4: return launch_mac_r<4>(R, coef, L, grid, lds, st);
-    case 10: return launch_mac_r<10>(R, coef, L, grid, lds, st);
+    case 2: return launch_mac_r<2>(R, mode, L, grid, lds, st);
+    case 3: return launch_mac_r<3>(R, mode, L, grid, lds, st);
+    case 4: return launch_mac_r<4>(R, mode, L, grid, lds, st);
+    case 10: return launch_mac_r<10>(R, mode, L, grid, lds, st);
 #if MEMO_EC_MAC_EXTRA_KC
-    case 6: return launch_mac_r4<6>(R, coef, L, grid, lds, st);
-    case 12: return launch_mac_r4<12>(R, coef, L, grid, lds, st);
-    case 14: return launch_mac_r4<14>(R, coef, L, grid, lds, st);
+    case 6: return launch_mac_r4<6>(R, mode, L, grid, lds, st);
+    case 12: return launch_mac_r4<12>(R, mode, L, grid, lds, st);
+    case 14: return launch_mac_r4<14>(R, mode, L, grid, lds, st);
 #endif
-    case 16: return launch_mac_r<16>(R, coef, L, grid, lds, st);
+    case 16: return launch_mac_r<16>(R, mode, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1210,6 +1616,23 @@ hipError_t launch_gather(const GatherArgs& a, hipStream_t st) {
   if (grid > 65536) grid = 65536;
   hipLaunchKernelGGL(gather_kernel, dim3((uint32_t)grid), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+// LW0(i) = log sigma(i) - log Pall(i) mod 255 (decode_coef_kernel's
+// stage_lw0), i < k + m, for the fused rebuild; zero past k + m.
+void lw0_host(int k, int m, uint8_t* out) {
+  const int nt = k + m;
+  for (int i = 0; i < 128; ++i) out[i] = 0;
+  for (int i = 0; i < nt && i < 128; ++i) {
+    uint32_t ls = 0, lp = 0;
+    for (int j = 0; j < nt; ++j) {
+      if (j == i) continue;
+      const uint32_t v = kGfHost.log[i ^ j];
+      lp += v;
+      if (j < k) ls += v;
+    }
+    out[i] = (uint8_t)((ls % 255 + 255 - lp % 255) % 255);
+  }
 }
 
 const uint8_t* host_gf_log() { return kGfHost.log; }

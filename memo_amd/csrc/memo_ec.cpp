@@ -42,6 +42,11 @@ struct memo_ec_ctx {
     uint32_t* dev;
   };
   std::vector<TabEntry> enc_tabs;  // cached encode images per (k, m, R, kpad)
+  struct Lw0Entry {
+    int k, m;
+    uint32_t* dev;
+  };
+  std::vector<Lw0Entry> lw0_tabs;  // cached LW0 tables per (k, m) (fused rebuild)
   // host pipeline: device slots and pinned bounce buffers
   uint8_t* d_slot[3] = {nullptr, nullptr, nullptr};
   size_t slot_cap = 0;
@@ -89,8 +94,8 @@ int check_km(int k, int m) {
 struct Plan {
   MacSeg seg{};
   int KC = 4, R = 1;
-  bool coef = false;  // tables built from per-block coefficient rows (rebuild)
-  size_t lds = 0;     // LDS bytes of this segment's table sets
+  int mode = MAC_ENCODE;  // MacMode: encode image / decode rows in HBM / fused decode
+  size_t lds = 0;         // LDS bytes of this segment's table sets (+ decode workspace)
 };
 
 uint32_t kpad_of(uint32_t kin, int KC) { return (kin + KC - 1) / KC * KC; }
@@ -101,18 +106,21 @@ uint64_t sets_per_tile(uint64_t C) { return (MAC_TILE - 1 + C - 1) / C + 1; }
 Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* in,
                   uint64_t in_bs, uint64_t in_ss, uint8_t* out, uint64_t out_bs, uint64_t out_ss,
                   const uint32_t* tab, uint64_t tab_bs_dw, int KC, int R,
-                  const uint8_t* coef = nullptr, uint64_t coef_bs = 0, uint32_t coef_rows = 0) {
+                  const uint8_t* coef = nullptr, uint64_t coef_bs = 0, uint32_t coef_rows = 0,
+                  bool fused = false) {
   Plan p;
   p.KC = KC;
   p.R = R;
-  p.coef = coef != nullptr;
+  // fused: per-block coefficients (coef_bs = e * k) the tile decodes itself
+  p.mode = fused ? MAC_FUSED : coef ? MAC_ROWS : MAC_ENCODE;
+  const bool per_coef = p.mode != MAC_ENCODE;
   MacSeg& s = p.seg;
   s.in = in; s.out = out; s.tab = tab;
   s.in_bstride = in_bs; s.in_sstride = in_ss;
   s.out_bstride = out_bs; s.out_sstride = out_ss;
   s.tab_bstride = tab_bs_dw;
   s.coef = coef; s.coef_bstride = coef_bs; s.coef_rows = coef_rows;
-  s.coef_dense = coef && coef_bs != 0 && coef_rows == (uint32_t)R &&
+  s.coef_dense = coef && !fused && coef_bs != 0 && coef_rows == (uint32_t)R &&
                  kin == kpad_of(kin, KC) && coef_bs == (uint64_t)R * kin;
   s.n = n; s.kin = kin; s.r = r;
   s.kpad = kpad_of(kin, KC);
@@ -120,15 +128,15 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   // LDS per table set: 8-dword images, or (rebuild, MAC_COEF_SOA) 16-B q +
   // 4-B lo per slot plus one pad slot (ec_kernels.hip: put_image)
   const size_t per = (size_t)R * s.kpad;
-  const bool soa = coef != nullptr && MAC_COEF_SOA;
+  const bool soa = per_coef && MAC_COEF_SOA;
   const size_t set_bytes = soa ? (per + 1) * 20 : per * 32;
   const uint64_t C = s.chunks;
   uint64_t sets;
-  if (coef ? coef_bs == 0 : tab_bs_dw == 0) {  // one table set for every block
+  if (per_coef ? coef_bs == 0 : tab_bs_dw == 0) {  // one table set for every block
     s.flat = 1;
     sets = 1;
   } else if (sets_per_tile(C) * set_bytes <= kLdsBudget &&
-             (!coef || sets_per_tile(C) * per <= 256u * MAC_COEF_REGS)) {
+             (!per_coef || sets_per_tile(C) * per <= 256u * MAC_COEF_REGS)) {
     // (the hot path stages at most MAC_COEF_REGS coefficients per lane)
     s.flat = 1;
     sets = sets_per_tile(C);
@@ -138,6 +146,13 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   }
   p.lds = sets * set_bytes;
   s.lo_dw = soa ? (uint32_t)(sets * (per + 1) * 4) : 0u;
+  if (fused) {
+    // decode workspace: the LDS phases' (chunk loop) or 4 waves' GF copies
+    // (wave-local decode on the hot path), whichever the kernel takes
+    s.ws_dw = (uint32_t)(p.lds / 4);
+    p.lds += std::max<size_t>(dec_ws_bytes((uint32_t)sets, kin, r),
+                                 (MAC_TILE / 64) * DEC_WAVE_BYTES);
+  }
   if (s.flat) {
     s.tiles = (n * C + MAC_TILE - 1) / MAC_TILE;
     s.tiles_per_block = 0;
@@ -173,10 +188,9 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   L.nseg = 0;
   uint64_t wg = 0;
   size_t lds = 0;
-  const int KC = plans[0].KC, R = plans[0].R;
-  const bool coef = plans[0].coef;
+  const int KC = plans[0].KC, R = plans[0].R, mode = plans[0].mode;
   for (auto& p : plans) {
-    if (p.KC != KC || p.R != R || p.coef != coef) return MEMO_EC_EINVAL;
+    if (p.KC != KC || p.R != R || p.mode != mode) return MEMO_EC_EINVAL;
     if (p.seg.tiles == 0) continue;
     wg = (wg + 7) / 8 * 8;  // segments start on an XCD-round boundary
     p.seg.wg_begin = (uint32_t)wg;
@@ -192,7 +206,7 @@ int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
   for (uint32_t i = 0; i < L.nseg; ++i) min_tiles = std::min<uint64_t>(min_tiles, L.seg[i].tiles);
   L.xcd = min_tiles >= xcd_min_tiles() ? 1u : 0u;
   if (lds > 160 * 1024) return MEMO_EC_ERANGE;
-  return hip_rc(launch_mac(KC, R, coef, L, (uint32_t)wg, lds, st));
+  return hip_rc(launch_mac(KC, R, mode, L, (uint32_t)wg, lds, st));
 }
 
 // Cached device table image of the Cauchy parity rows of (k, m).
@@ -218,6 +232,39 @@ int encode_tables(memo_ec_ctx* ctx, int k, int m, int R, int KC, const uint32_t*
   ctx->enc_tabs.push_back({k, m, R, kpad, dev});
   *out = dev;
   return MEMO_EC_OK;
+}
+
+// Cached device LW0 table of (k, m) (fused rebuild).
+int lw0_table(memo_ec_ctx* ctx, int k, int m, const uint32_t** out) {
+  for (auto& e : ctx->lw0_tabs)
+    if (e.k == k && e.m == m) {
+      *out = e.dev;
+      return MEMO_EC_OK;
+    }
+  uint8_t img[128];
+  lw0_host(k, m, img);
+  uint32_t* dev = nullptr;
+  HIPCHK(hipMalloc(&dev, sizeof img));
+  hipError_t e = hipMemcpy(dev, img, sizeof img, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(dev);
+    return hip_rc(e);
+  }
+  ctx->lw0_tabs.push_back({k, m, dev});
+  *out = dev;
+  return MEMO_EC_OK;
+}
+
+// 0 (default): the two-kernel rebuild, decode_coef_kernel rows through HBM
+// + gf_mac_kernel; 1: one fused launch (gf_rebuild_kernel) whose tiles
+// derive their blocks' rows themselves (MEMO_EC_REBUILD_FUSED, read per
+// call).  Measured (profiles/r02_rebuild_pmc.md): the MAC is ~75% VALU-busy,
+// and the fused decode's VALU/LDS work costs more than the decode kernel
+// and the rows' HBM round trip it removes -- C3 1054 vs 1012 us, 4 KiB
+// RS(10,4) 1239 vs 1186 us, 4 KiB RS(16,4) 1059 vs 1063 us.
+bool rebuild_fused() {
+  const char* p = std::getenv("MEMO_EC_REBUILD_FUSED");
+  return p && std::atoi(p) != 0;
 }
 
 int sync_pipeline(memo_ec_ctx* ctx);
@@ -407,18 +454,37 @@ int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint
   return MEMO_EC_OK;
 }
 
-// Device-resident rebuild on stream st: closed-form decode rows (one lane per
-// block), then the MAC, which builds each block's product tables in LDS from
-// its rows.  `scratch` has room for tab_bytes(k, e, n).
+// Device-resident rebuild on stream st.  Fused (default): one launch of
+// gf_rebuild_kernel, whose tiles derive their blocks' decode rows from the
+// indices.  Two-kernel: closed-form decode rows (one lane per block) into
+// `scratch` (room for tab_bytes(k, e, n)), then the MAC, which builds each
+// block's product tables in LDS from its rows.  Faults go to `status`.
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
-                   void* scratch, hipStream_t st, uint32_t* status = nullptr) {
+                   bool fused, void* scratch, hipStream_t st, uint32_t* status) {
   const int R = mac_rbound(e), KC = mac_kchunk(k, R);
   const size_t step = max_blocks_per_launch(S);
+  if (fused) {
+    const uint32_t* lw0 = nullptr;
+    if (int rc = lw0_table(ctx, k, m, &lw0)) return rc;
+    for (size_t b0 = 0; b0 < n; b0 += step) {
+      const size_t cnt = std::min(step, n - b0);
+      Plan p = plan_segment((uint32_t)k, (uint32_t)e, S, cnt, surv + b0 * (size_t)k * S,
+                            (uint64_t)k * S, S, out + b0 * (size_t)e * S, (uint64_t)e * S, S,
+                            nullptr, 0, KC, R, nullptr, (uint64_t)e * k, (uint32_t)e, true);
+      p.seg.sidx = surv_idx + b0 * (size_t)k;
+      p.seg.lidx = lost_idx + b0 * (size_t)e;
+      p.seg.lw0 = lw0;
+      p.seg.status = status;
+      p.seg.m = (uint32_t)m;
+      std::vector<Plan> plans{p};
+      if (int rc = launch_plans(plans, st)) return rc;
+    }
+    return MEMO_EC_OK;
+  }
   uint8_t* rows = static_cast<uint8_t*>(scratch);
   const uint64_t row_b = (uint64_t)e * k;
-  DecodeArgs a{surv_idx, lost_idx, rows, status ? status : ctx->d_status, n, (uint32_t)k,
-               (uint32_t)m, (uint32_t)e, 0};
+  DecodeArgs a{surv_idx, lost_idx, rows, status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0};
   HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
@@ -432,8 +498,14 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
   return MEMO_EC_OK;
 }
 
-// Rebuild scratch for n blocks: their decode rows, e x k bytes each.
-size_t tab_bytes(int k, int e, size_t n) { return n * (size_t)e * k; }
+// Rebuild scratch for n blocks: their decode rows, e x k bytes each (the
+// two-kernel path; the fused one needs none).
+size_t tab_bytes(int k, int e, size_t n, bool fused) { return fused ? 0 : n * (size_t)e * k; }
+
+// Deferred-error words in ctx->d_status: device-resident calls (reported by
+// memo_ec_synchronize) and the host-memory copy pipeline (reported by the
+// call itself) each have their own, so neither consumes the other's fault.
+constexpr size_t kStatusDevice = 0, kStatusPipeline = 16;
 
 // Host-memory pipeline over batches of nb blocks.  Batch i uses slot i % 3:
 //   in(slot, b0, cnt, st)   host staging + HtoD copies on st
@@ -592,6 +664,7 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
     if (p) (void)hipHostFree(p);
   if (c->d_tabs) (void)hipFree(c->d_tabs);
   for (auto& e : c->enc_tabs) (void)hipFree(e.dev);
+  for (auto& e : c->lw0_tabs) (void)hipFree(e.dev);
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
   for (int i = 0; i < kSlots; ++i)
@@ -691,7 +764,8 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   if (n == 0 || e == 0) return MEMO_EC_OK;
   if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
-  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0};
+  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status + kStatusDevice, n, (uint32_t)k, (uint32_t)m,
+               (uint32_t)e, 0};
   return hip_rc(launch_decode_coef(a, c->stream));
 }
 
@@ -704,10 +778,11 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
+  const bool fused = rebuild_fused();
   if (where == MEMO_EC_DEVICE) {
-    if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
-    if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, c->d_tabs,
-                                c->stream))
+    if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
+    if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, fused, c->d_tabs,
+                                c->stream, c->d_status + kStatusDevice))
       return rc;
     // marks the scratch busy until this rebuild is done (host calls check it)
     return hip_rc(hipEventRecord(c->ev_order, c->stream));
@@ -730,7 +805,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
     // pinned buffers); the status word rides in the slot too.
     const size_t slot = n * (in_b + out_b + idx_b) + 64;
     if (int rc = ensure_slots(c, 0, slot)) return rc;
-    if (int rc = ensure_tabs(c, tab_bytes(k, e, n))) return rc;
+    if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
     uint8_t* h = c->h_slot[0];
     uint8_t* h_sidx = h + n * (in_b + out_b);
     uint8_t* h_lidx = h_sidx + n * k;
@@ -745,7 +820,8 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       sv = h;
       ov = h + n * in_b;
     }
-    if (int rc = rebuild_device(c, k, m, S, n, h_sidx, sv, h_lidx, e, ov, c->d_tabs, c->sk, h_st))
+    if (int rc = rebuild_device(c, k, m, S, n, h_sidx, sv, h_lidx, e, ov, fused, c->d_tabs, c->sk,
+                                h_st))
       return rc;
     HIPCHK(hipStreamSynchronize(c->sk));
     if (!pinned) par_memcpy(out, ov, n * out_b);
@@ -759,7 +835,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e]
   const size_t slot = nb * (in_b + out_b + idx_b);
   if (int rc = ensure_slots(c, slot, slot)) return rc;
-  const size_t tabs = tab_bytes(k, e, nb);
+  const size_t tabs = tab_bytes(k, e, nb, fused);
   if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
   const int rc = run_pipeline(
@@ -779,8 +855,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       },
       [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
         uint8_t* d = c->d_slot[s];
-        return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out,
-                              reinterpret_cast<uint8_t*>(c->d_tabs) + (size_t)s * tabs, st);
+        return rebuild_device(c, k, m, S, cnt, d + o_sidx, d, d + o_lidx, e, d + o_out, fused,
+                              reinterpret_cast<uint8_t*>(c->d_tabs) + (size_t)s * tabs, st,
+                              c->d_status + kStatusPipeline);
       },
       [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + o_out;
@@ -788,7 +865,8 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
         // the deferred-error word rides behind the last batch's output, so
         // reading it costs no extra round trip
         if (b0 + cnt == n)
-          HIPCHK(hipMemcpyAsync(c->h_status, c->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost,
+          HIPCHK(hipMemcpyAsync(c->h_status, c->d_status + kStatusPipeline, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost,
                                 st));
         return MEMO_EC_OK;
       },
@@ -798,7 +876,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (rc) return rc;
   const uint32_t st = *c->h_status;
   if (st) {
-    HIPCHK(hipMemsetAsync(c->d_status, 0, sizeof(uint32_t), c->sd));
+    HIPCHK(hipMemsetAsync(c->d_status + kStatusPipeline, 0, sizeof(uint32_t), c->sd));
     HIPCHK(hipStreamSynchronize(c->sd));
   }
   int drc = c->deferred;

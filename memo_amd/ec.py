@@ -116,6 +116,27 @@ def erasures(seed, first_block, n, k, m, e):
     return s, l[:, :e].copy()
 
 
+def rebuild_path():
+    """Which device rebuild the library runs (memo_ec.cpp rebuild_fused):
+    'rows' (default) -- decode_coef_kernel rows through HBM, then
+    gf_mac_kernel; 'fused' -- one gf_rebuild_kernel launch whose tiles derive
+    their blocks' decode rows from the indices (MEMO_EC_REBUILD_FUSED=1)."""
+    v = os.environ.get("MEMO_EC_REBUILD_FUSED")
+    return "fused" if v is not None and _atoi(v) != 0 else "rows"
+
+
+def _atoi(v):
+    try:
+        return int(v.strip().split()[0])
+    except (ValueError, IndexError):
+        return 0
+
+
+def rebuild_kernel_name():
+    return {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
+            "rows": "decode_coef_kernel + gf_mac_kernel (rows through HBM)"}[rebuild_path()]
+
+
 def _is_torch(x):
     return type(x).__module__.startswith("torch")
 

@@ -37,3 +37,12 @@ def codec():
     c = ec.Codec(0)
     yield c
     c.close()
+
+
+@pytest.fixture(params=["fused", "rows"])
+def rebuild_path(request, monkeypatch):
+    """Run a rebuild test on both device rebuild paths: the fused
+    gf_rebuild_kernel (default) and the two-kernel decode_coef_kernel +
+    gf_mac_kernel path (MEMO_EC_REBUILD_FUSED=0, read per call)."""
+    monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", "1" if request.param == "fused" else "0")
+    return request.param

@@ -40,7 +40,7 @@ def test_fill_matches_oracle(codec, O):
         assert np.array_equal(host(d), O.fill_blocks(SEED, 3, 5, B, k, S)), (B, k)
 
 
-def test_golden_cases(codec, golden, O):
+def test_golden_cases(codec, golden, O, rebuild_path):
     for ci, row in enumerate(golden["cases"]):
         k, m, B, fb, nb, e, S = map(int, row)
         d = fill(codec, fb, nb, B, k, S)
@@ -68,7 +68,7 @@ CONFIGS = [(1, 1), (2, 1), (3, 2), (4, 2), (5, 3), (6, 3), (6, 6), (8, 5), (10, 
 
 
 @pytest.mark.parametrize("k,m", CONFIGS)
-def test_encode_rebuild_vs_oracle(codec, O, k, m):
+def test_encode_rebuild_vs_oracle(codec, O, k, m, rebuild_path):
     rng = np.random.default_rng(k * 100 + m)
     for B in [64 * k, 4096, 12345, 300000]:
         S = O.shard_size(B, k)
@@ -90,7 +90,7 @@ def test_encode_rebuild_vs_oracle(codec, O, k, m):
             assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
 
 
-def test_batches_split_across_launches(codec, O, monkeypatch):
+def test_batches_split_across_launches(codec, O, monkeypatch, rebuild_path):
     """A batch larger than one launch's grid is split into several MAC
     launches (memo_ec.cpp max_blocks_per_launch); the bound is lowered so the
     split happens at a testable size.  Encode and rebuild, device and host."""
@@ -139,7 +139,7 @@ def test_c1_full_size_vs_oracle(codec, O):
 
 
 @pytest.mark.parametrize("k,m", [(3, 2), (4, 2)])
-def test_every_erasure_pattern_in_one_batch(codec, O, k, m):
+def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
     """Each block of the batch has a different erasure pattern (per-block
     decode tables in one launch); all patterns of size m."""
     pats = list(itertools.combinations(range(k + m), m))
@@ -206,7 +206,7 @@ def test_one_huge_ragged_block(codec, O):
     assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
 
 
-def test_small_blocks_many_per_tile(codec, O):
+def test_small_blocks_many_per_tile(codec, O, rebuild_path):
     # 4 KiB blocks with k=16: S=256, 16 columns per block, tables for ~17
     # blocks per tile in the rebuild kernel.
     k, m, B, n = 16, 4, 4096, 300
@@ -307,7 +307,7 @@ def test_small_host_calls(codec, O, zc_kb, monkeypatch):
             assert np.array_equal(out, O.gather(k, m, S, data, want, l)), (B, n, e)
 
 
-def test_singular_survivors_reported(codec):
+def test_singular_survivors_reported(codec, rebuild_path):
     from memo_amd import ec
     k, m, S, n = 4, 2, 64, 2
     surv = dev(np.array([[0, 1, 2, 3], [0, 1, 1, 2]], np.uint8))  # block 1: duplicate
@@ -345,7 +345,7 @@ def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
 
 
 @pytest.mark.parametrize("B,n", [(1 << 16, 40), (4096, 5)])
-def test_singular_survivors_reported_host_paths(codec, O, monkeypatch, B, n):
+def test_singular_survivors_reported_host_paths(codec, O, monkeypatch, B, n, rebuild_path):
     """Host-memory rebuilds report a bad survivor set from any pipeline batch
     (the status word is read behind the last batch) or from a small
     zero-copy call (status word in the pinned slot), the good blocks are
@@ -391,7 +391,7 @@ def test_noops_and_argument_errors(codec):
     codec.synchronize()
 
 
-def test_full_size_c2_c3_round_trip(codec, O):
+def test_full_size_c2_c3_round_trip(codec, O, rebuild_path):
     """BASELINE.json C2/C3 at full size (4096 x 1 MiB, RS(10,4), e=4):
     sampled blocks bit-exact vs the oracle; every block's 4 erased shards
     rebuilt bit-exact (device-side comparison)."""
@@ -586,3 +586,85 @@ def test_concurrent_host_calls_from_threads(O):
     for t in ts:
         t.join()
     assert not errs, errs
+
+
+@pytest.mark.parametrize("k,m,B", [(10, 4, 4096), (16, 4, 4096), (4, 2, 100), (3, 2, 5000),
+                                   (2, 2, 64), (5, 3, 4096), (12, 4, 7000), (20, 8, 3000),
+                                   (64, 16, 5000), (10, 4, 300000)])
+def test_fused_rebuild_random_orders(codec, O, k, m, B):
+    """The fused rebuild (each tile decodes its blocks' rows itself) on
+    per-block random survivor orders and lost sets that mix data, parity and
+    survivor shards (unit rows), over tiles holding 1 to 65 blocks (S = 64
+    packs 4 columns per block) and through the generic chunk loop (k = 5,
+    20, 64), against the true shards."""
+    rng = np.random.default_rng(k * 7 + m + B)
+    S = O.shard_size(B, k)
+    n = 300
+    data = O.fill_blocks(SEED, 11, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    for e in sorted({1, m}):
+        surv = np.stack([rng.permutation(k + m)[:k] for _ in range(n)]).astype(np.uint8)
+        lost = np.stack([rng.permutation(k + m)[:e] for _ in range(n)]).astype(np.uint8)
+        sv = O.gather(k, m, S, data, par, surv)
+        out = empty(n, e * S)
+        codec.rebuild(k, m, dev(surv), dev(sv), dev(lost), out)
+        codec.synchronize()
+        assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost)), (k, m, B, e)
+
+
+@pytest.mark.parametrize("B", [4096, 1 << 20])
+def test_fused_invalid_sets_zero_only_that_block(codec, O, B):
+    """Duplicate survivors, a survivor index >= k+m and a lost index >= k+m
+    zero that block's output only (its neighbours in the same tile are
+    rebuilt) and raise ESINGULAR once."""
+    from memo_amd import ec
+    k, m, e = 10, 4, 2
+    S = O.shard_size(B, k)
+    n = 6
+    data = O.fill_blocks(SEED, 3, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    surv = np.array([list(range(10)), [0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [0, 1, 2, 3, 4, 5, 6, 7, 8, 14],
+                     [13, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(10)), [12, 1, 2, 3, 4, 5, 6, 7, 8, 9]],
+                    np.uint8)
+    lost = np.array([[10, 11], [10, 11], [10, 11], [0, 12], [11, 14], [0, 9]], np.uint8)
+    sv = O.gather(k, m, S, data, par, np.minimum(surv, k + m - 1))
+    out = empty(n, e * S)
+    codec.rebuild(k, m, dev(surv), dev(sv), dev(lost), out)
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.synchronize()
+    assert ei.value.code == -4
+    got = host(out).reshape(n, e * S)
+    for b in (1, 2, 4):
+        assert not got[b].any(), b
+    for b in (0, 3, 5):
+        assert np.array_equal(got[b], O.gather(k, m, S, data[b:b + 1], par[b:b + 1],
+                                               lost[b:b + 1]).reshape(-1)), b
+    codec.synchronize()
+
+
+def test_device_fault_does_not_leak_into_host_pipeline(O, monkeypatch):
+    """A device rebuild with a bad survivor set, then a good host-memory
+    rebuild through the copy pipeline on the same ctx: the host call
+    succeeds (its own status word), and the device fault is still reported
+    by the next synchronize."""
+    from memo_amd import ec
+    k, m, B, n = 4, 2, 1 << 16, 40
+    S = O.shard_size(B, k)
+    monkeypatch.setenv("MEMO_EC_PIPE_MB", "1")
+    monkeypatch.setenv("MEMO_EC_ZC_KB", "0")
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    s, l = O.erasures(SEED, 0, n, k, m, 1)
+    surv = O.gather(k, m, S, data, par, s)
+    want = O.gather(k, m, S, data, par, l)
+    bad = s.copy()
+    bad[5, 1] = bad[5, 0]
+    with ec.Codec(0) as c:
+        c.rebuild(k, m, dev(bad), dev(surv), dev(l), empty(n, S))   # device, async, faulty
+        out = np.zeros((n, S), np.uint8)
+        c.rebuild(k, m, s, surv, l, out)                             # host pipeline, good
+        assert np.array_equal(out, want.reshape(n, S))
+        with pytest.raises(ec.MemoECError) as ei:
+            c.synchronize()
+        assert ei.value.code == -4
+        c.synchronize()

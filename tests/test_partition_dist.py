@@ -77,24 +77,100 @@ def test_two_rank_partition_gloo():
     assert np.array_equal(np.concatenate(parts), whole)
 
 
-@pytest.mark.gpu
-def test_bench_two_ranks_on_one_gpu():
-    """bench.py's N>1 path end to end on the one GPU of a test box: two
-    ranks under torch.distributed.run (gloo for the barrier/max, both ranks
-    on cuda:0), each encoding its own block range; rank 0 prints one JSON
-    line with the whole-job value.  The 8-GPU RCCL run is the driver's."""
-    import json
-    import subprocess
+def test_launch_local_ranks_env(tmp_path):
+    """bench.py's own launcher (no torchrun): N children started together,
+    each with its RANK / LOCAL_RANK / WORLD_SIZE and one rendezvous port;
+    a failing rank fails the launch."""
     import sys
-    port = _free_port()
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--steps", "3", "--warmup", "2",
-           "--blocks", "64", "--no-cpu", "--no-e2e"]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    from memo_amd.partition import launch_local_ranks
+    script = tmp_path / "child.py"
+    out = tmp_path / "out"
+    out.mkdir()
+    script.write_text(
+        "import os, sys\n"
+        "e = os.environ\n"
+        "open(os.path.join(sys.argv[1], e['RANK']), 'w').write("
+        "'%s %s %s %s' % (e['LOCAL_RANK'], e['WORLD_SIZE'], e['MASTER_ADDR'], e['MASTER_PORT']))\n"
+        "sys.exit(3 if len(sys.argv) > 2 and sys.argv[2] == e['RANK'] else 0)\n")
+    assert launch_local_ranks(str(script), [str(out)], 3) == 0
+    got = {f.name: f.read_text().split() for f in out.iterdir()}
+    assert sorted(got) == ["0", "1", "2"]
+    assert {v[3] for v in got.values()} == {got["0"][3]}
+    for r, v in got.items():
+        assert v[0] == r and v[1] == "3" and v[2] == "127.0.0.1"
+    assert launch_local_ranks(str(script), [str(out)], 2, same_device=True) == 0
+    assert all((out / r).read_text().split()[0] == "0" for r in ("0", "1"))
+    assert launch_local_ranks(str(script), [str(out), "1"], 2) == 3
+
+
+def test_bench_assemble_per_rank_fields():
+    """The bench line for N ranks: value = all payload / the job wall time,
+    per-GPU rates from each rank's own kernel time, node sum over the
+    slowest rank, both directions' roofline fractions."""
+    import bench
+    args = bench.parse(["--gpus", "2", "--blocks", "4096", "--steps", "10"])
+    S = 104896
+    n, B, K = 4096, 1 << 20, 10
+
+    def row(r, enc_ms, reb_ms):
+        return {"rank": r, "device": r, "warmup_steps_run": 40,
+                "payload_bytes": n * B * 2 * K, "device_seconds": (enc_ms + reb_ms) * K * 1e-3,
+                "encode": bench.kstats([enc_ms] * K, 14 * S * n),
+                "rebuild": bench.kstats([reb_ms] * K, 14 * S * n),
+                "rebuild_bit_exact": True, "rebuild_kernel": "gf_rebuild_kernel"}
+    rows = [row(0, 1.0, 1.1), row(1, 1.05, 1.2)]
+    res = bench.assemble(args, 2, rows, 0.05, S)
+    assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 8192
+    assert res["value"] == round(2 * n * B * 2 * K / 0.05 / 2**30, 3)
+    pg = res["ranks"]["per_gpu"]
+    assert [p["rank"] for p in pg] == [0, 1]
+    assert pg[0]["GiBs"] == round(n * B * 2 / 2.1e-3 / 2**30, 3)
+    assert res["ranks"]["node_sum_GiBs"] == round(2 * n * B * 2 * K / (2.25e-3 * K) / 2**30, 3)
+    assert res["roofline"]["kernel_ms_max_over_ranks"] == 1.05
+    assert res["roofline"]["frac"] == round(14 * S * n / 1e-3 / 1e9 / 8000, 4)
+    assert res["roofline_rebuild"]["kernel"] == "gf_rebuild_kernel"
+    assert res["rebuild"]["round_trip_bit_exact"]
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert key in res
+
+
+def _bench_json(r):
+    import json
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
-    res = json.loads(lines[0])
+    return json.loads(lines[0])
+
+
+BENCH_SMALL = ["--gpus", "2", "--same-device", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
+               "--blocks", "64", "--no-cpu", "--no-e2e", "--no-small"]
+
+
+@pytest.mark.gpu
+def test_bench_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no external launcher starts both ranks
+    itself (both on cuda:0 here; one per GPU on a node), each encoding and
+    rebuilding its own 64 blocks; rank 0 prints one line."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + BENCH_SMALL,
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    res = _bench_json(r)
+    assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 128
+    assert res["value"] > 0 and res["rebuild"]["round_trip_bit_exact"]
+    assert len(res["ranks"]["per_gpu"]) == 2 and res["ranks"]["node_sum_GiBs"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_under_torchrun():
+    """The driver's N>1 launch: torch.distributed.run starts the ranks, and
+    bench.py uses them (gloo for the barrier/max, no RCCL)."""
+    import subprocess
+    import sys
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py")] + BENCH_SMALL
+    res = _bench_json(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT))
     assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 128
     assert res["value"] > 0 and res["rebuild"]["round_trip_bit_exact"]
