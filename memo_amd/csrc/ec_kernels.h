@@ -134,6 +134,7 @@ struct DecodeArgs {
   uint64_t n;
   uint32_t k, m, e;
   uint32_t pitch;         // decode_coef_kernel: LDS row-staging pitch (set by the launcher)
+  const uint32_t* lw0;    // LW0 table of (k, m) (lw0_host; 128 bytes); null: computed per workgroup
 };
 
 struct Sha256Args {

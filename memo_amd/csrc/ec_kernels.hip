@@ -1194,6 +1194,157 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   }
 }
 
+// Per-block decode for an exact k = K <= 16 (the common codes): K + m <= 32,
+// so a block's survivor set is one 32-bit mask; its m non-survivors are
+// extracted once into registers (ctz), every loop is unrolled at compile
+// time (rows r < e by uniform predicates), the rows are packed into dwords
+// before they are staged in LDS (e*K/4 dword stores instead of e*K byte
+// stores), and LW0 comes from the host's per-code table.  Same results as
+// decode_coef_kernel (tests/test_gpu_parity.py); about half its VALU work.
+template <int K>
+__global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
+  static_assert(K <= 16, "one 32-bit survivor mask: K + MEMO_EC_MAX_M <= 32");
+  __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
+  __shared__ uint32_t s_lw0[32];
+  extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
+  const uint8_t* ex = lg + 256;
+  const uint8_t* lw0 = reinterpret_cast<const uint8_t*>(s_lw0);
+  const uint32_t m = a.m, e = a.e, nt = K + a.m;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t b = b0 + tid;
+  const bool live = b < a.n;
+  // The block's indices, with the widest loads their alignment allows (the
+  // kernel is short: its first loads are a visible part of it).
+  uint32_t sv[K], lv[MEMO_EC_MAX_M];
+  const uintptr_t sa = reinterpret_cast<uintptr_t>(a.surv_idx);
+  if (K % 4 == 0 && (sa & 3) == 0) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(a.surv_idx + b * K);
+#pragma unroll
+    for (int w = 0; w < K / 4; ++w) {
+      const uint32_t x = live ? p[w] : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sv[4 * w + j] = (x >> (8 * j)) & 0xFFu;
+    }
+  } else if (K % 2 == 0 && (sa & 1) == 0) {
+    const uint16_t* p = reinterpret_cast<const uint16_t*>(a.surv_idx + b * K);
+#pragma unroll
+    for (int w = 0; w < K / 2; ++w) {
+      const uint32_t x = live ? p[w] : 0u;
+      sv[2 * w] = x & 0xFFu;
+      sv[2 * w + 1] = x >> 8;
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < K; ++t) sv[t] = live ? a.surv_idx[b * K + t] : 0u;
+  }
+  if ((e & 3) == 0 && (reinterpret_cast<uintptr_t>(a.lost_idx) & 3) == 0) {
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(a.lost_idx + b * e);
+#pragma unroll
+    for (int w = 0; w < MEMO_EC_MAX_M / 4; ++w) {
+      const uint32_t x = (live && (uint32_t)(4 * w) < e) ? p[w] : 0u;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) lv[4 * w + j] = (x >> (8 * j)) & 0xFFu;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < MEMO_EC_MAX_M; ++r) lv[r] = (live && (uint32_t)r < e) ? a.lost_idx[b * e + r] : 0u;
+  }
+  {
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&kGf);
+    for (uint32_t i = tid; i < kGfDwords; i += 256) s_gf[i] = src[i];
+    if (tid < 32) s_lw0[tid] = a.lw0[tid];
+  }
+  __syncthreads();
+  const uint32_t ek = e * K;
+  uint32_t* out = reinterpret_cast<uint32_t*>(s_out + tid * a.pitch);
+  if (live) {
+    // survivor set: range and duplicates
+    uint32_t mask = 0;
+    bool bad = false;
+#pragma unroll
+    for (int t = 0; t < K; ++t) {
+      const uint32_t v = sv[t], bit = 1u << (v & 31);
+      bad |= v >= nt || (mask & bit) != 0;
+      mask |= bit;
+    }
+    // the m non-survivors, in registers
+    uint32_t comp = ~mask & (nt >= 32 ? ~0u : (1u << nt) - 1u);
+    uint32_t cl[MEMO_EC_MAX_M];
+#pragma unroll
+    for (int q = 0; q < MEMO_EC_MAX_M; ++q) {
+      cl[q] = 0;
+      if ((uint32_t)q < m) {
+        cl[q] = __builtin_ctz(comp | 0x80000000u);  // a faulty set may run out: 31
+        comp &= comp - 1;
+      }
+    }
+    // log W_t = LW0(s_t) + sum_c log(s_t ^ c)
+    uint32_t lw[K];
+#pragma unroll
+    for (int t = 0; t < K; ++t) lw[t] = lw0[sv[t] & 31];
+#pragma unroll
+    for (int q = 0; q < MEMO_EC_MAX_M; ++q)
+      if ((uint32_t)q < m) {
+#pragma unroll
+        for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]];
+      }
+#pragma unroll
+    for (int t = 0; t < K; ++t) lw[t] = mod255(lw[t]) + 255u;
+    // rows, packed 4 bytes per dword
+    uint32_t word = 0;
+#pragma unroll
+    for (int r = 0; r < MEMO_EC_MAX_M; ++r) {
+      if ((uint32_t)r < e) {
+        const uint32_t l = lv[r];
+        bad |= l >= nt;
+        const bool unit = (mask >> (l & 31)) & 1u;
+        uint32_t acc = lw0[l & 31];
+#pragma unroll
+        for (int q = 0; q < MEMO_EC_MAX_M; ++q)
+          if ((uint32_t)q < m) acc += lg[l ^ cl[q]];  // c == l adds log[0] = 0
+        const uint32_t llam = 255u - mod255(acc);   // log Lam_l, in 1..255
+#pragma unroll
+        for (int t = 0; t < K; ++t) {
+          // lw + llam - log(l ^ s_t) < 765
+          uint32_t v = unit ? (sv[t] == l ? 1u : 0u) : ex[lw[t] + llam - lg[l ^ sv[t]]];
+          v = bad ? 0u : v;
+          const int q = r * K + t;  // compile-time byte position
+          word |= v << (8 * (q & 3));
+          if ((q & 3) == 3) {
+            out[q >> 2] = word;
+            word = 0;
+          }
+        }
+      }
+    }
+    if ((ek & 3) != 0) out[ek >> 2] = word;  // the partial last dword
+    if (bad) {
+      for (uint32_t w = 0; w < (ek + 3) / 4; ++w) out[w] = 0;
+      if (a.status) *a.status = 1u;  // plain store: every writer stores 1
+    }
+  }
+  __syncthreads();
+  // this workgroup's rows are one contiguous range of nb * ek bytes
+  const uint64_t nb = a.n - b0 < 256 ? a.n - b0 : 256;
+  uint8_t* dst = a.rows + b0 * ek;
+  const uint32_t total = (uint32_t)nb * ek;
+  if ((ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) {
+    const uint32_t ekw = ek >> 2;
+    for (uint32_t w = tid; w < (total >> 2); w += 256) {
+      const uint32_t lb = w / ekw, off = w - lb * ekw;
+      reinterpret_cast<uint32_t*>(dst)[w] =
+          *reinterpret_cast<const uint32_t*>(s_out + lb * a.pitch + off * 4);
+    }
+  } else {
+    for (uint32_t x = tid; x < total; x += 256) {
+      const uint32_t lb = x / ek, off = x - lb * ek;
+      dst[x] = s_out[lb * a.pitch + off];
+    }
+  }
+}
+
 // Latency variant for small batches: L lanes per block (L = the power of two
 // >= k), lane t owns survivor column t.  The block's survivor bit set is
 // OR-reduced across its L lanes; each lane then needs only its own W_t
@@ -1586,6 +1737,21 @@ hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   pw |= 1u;
   a.pitch = 256u * pw * 4 <= 64 * 1024 ? pw * 4 : 0u;
   const size_t lds = a.pitch ? 256u * a.pitch : 0;
+  // exact-k kernels for the common codes (MEMO_EC_DECODE_EXACT=0: off; read
+  // per call, for A/B runs and tests)
+  const char* ex_env = std::getenv("MEMO_EC_DECODE_EXACT");
+  const bool exact = !ex_env || std::atoi(ex_env) != 0;
+  if (exact && a.pitch && a.lw0 && a.k + a.m <= 32) {
+    switch (a.k) {
+      case 4: hipLaunchKernelGGL(decode_rows_k_kernel<4>, dim3(grid), dim3(256), lds, st, a);
+        return hipGetLastError();
+      case 10: hipLaunchKernelGGL(decode_rows_k_kernel<10>, dim3(grid), dim3(256), lds, st, a);
+        return hipGetLastError();
+      case 16: hipLaunchKernelGGL(decode_rows_k_kernel<16>, dim3(grid), dim3(256), lds, st, a);
+        return hipGetLastError();
+      default: break;
+    }
+  }
   if (a.k <= 4)
     hipLaunchKernelGGL(decode_coef_kernel<4>, dim3(grid), dim3(256), lds, st, a);
   else if (a.k <= 10)

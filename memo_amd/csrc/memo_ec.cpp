@@ -484,7 +484,9 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
   }
   uint8_t* rows = static_cast<uint8_t*>(scratch);
   const uint64_t row_b = (uint64_t)e * k;
-  DecodeArgs a{surv_idx, lost_idx, rows, status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0};
+  const uint32_t* lw0 = nullptr;
+  if (int rc = lw0_table(ctx, k, m, &lw0)) return rc;
+  DecodeArgs a{surv_idx, lost_idx, rows, status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0, lw0};
   HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
@@ -764,8 +766,10 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   if (n == 0 || e == 0) return MEMO_EC_OK;
   if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
+  const uint32_t* lw0 = nullptr;
+  if (int rc = lw0_table(c, k, m, &lw0)) return rc;
   DecodeArgs a{surv_idx, lost_idx, rows, c->d_status + kStatusDevice, n, (uint32_t)k, (uint32_t)m,
-               (uint32_t)e, 0};
+               (uint32_t)e, 0, lw0};
   return hip_rc(launch_decode_coef(a, c->stream));
 }
 

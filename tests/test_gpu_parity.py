@@ -158,16 +158,19 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
 
 @pytest.mark.parametrize("k,m", [(1, 1), (3, 2), (4, 2), (7, 5), (10, 4), (16, 4), (20, 8),
                                  (33, 12), (64, 16)])
-@pytest.mark.parametrize("kernel", ["wide", "per_block"])
+@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_generic"])
 def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
     """Closed-form decode rows against the oracle's Gauss-Jordan rows
     C[lost] * inv(C[surv]): random survivor orders, lost shards that are
     data, parity or themselves survivors (unit rows), e = 1..m, over 700
     blocks (several workgroups).  Both kernels: column-per-lane
     (decode_coef_wide_kernel, small batches) and one lane per block
-    (decode_coef_kernel, forced by MEMO_EC_DECODE_WIDE_MAX=0)."""
-    if kernel == "per_block":
+    (forced by MEMO_EC_DECODE_WIDE_MAX=0: decode_rows_k_kernel for k in
+    {4, 10, 16}, decode_coef_kernel otherwise or with MEMO_EC_DECODE_EXACT=0)."""
+    if kernel != "wide":
         monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
+    if kernel == "per_block_generic":
+        monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
     rng = np.random.default_rng(k * 1000 + m)
     n = 700
     for e in sorted({1, (m + 1) // 2, m}):
@@ -320,13 +323,15 @@ def test_singular_survivors_reported(codec, rebuild_path):
     codec.synchronize()  # error is cleared
 
 
-@pytest.mark.parametrize("kernel", ["wide", "per_block"])
+@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_generic"])
 def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
     """Duplicate survivors, a survivor index >= k+m and a lost index >= k+m
     zero that block's rows (only that block's) and raise ESINGULAR once."""
     from memo_amd import ec
-    if kernel == "per_block":
+    if kernel != "wide":
         monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
+    if kernel == "per_block_generic":
+        monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
     k, m, e = 10, 4, 2
     surv = np.array([list(range(10)), [0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [0, 1, 2, 3, 4, 5, 6, 7, 8, 14],
                      [13, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(10))], np.uint8)
@@ -668,3 +673,54 @@ def test_device_fault_does_not_leak_into_host_pipeline(O, monkeypatch):
             c.synchronize()
         assert ei.value.code == -4
         c.synchronize()
+
+
+def _headline():
+    import json
+    import os
+    from conftest import ROOT
+    with open(os.path.join(ROOT, "tests", "golden", "rs_headline.json")) as f:
+        return json.load(f)
+
+
+def _sha(x):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["C2_C3", "C1", "small_16_4", "small_10_4", "C5_4MiB_4_2"])
+def test_headline_batches_vs_numpy_digests(codec, name, rebuild_path):
+    """Each headline batch (BASELINE.json C1/C2/C3, the 4 KiB rebuild_small
+    batches, 4 MiB RS(4,2)) runs whole on the GPU -- encode, then a rebuild
+    with the batch's random erasure patterns -- and its sample blocks' data,
+    parity and rebuilt shards match the SHA-256 digests of the independent
+    numpy restatement (tests/golden/rs_headline.json, make_headline.py)."""
+    import torch
+    from memo_amd import ec
+    bt = [b for b in _headline()["batches"] if b["name"] == name][0]
+    k, m, B, n, S = bt["k"], bt["m"], bt["block_bytes"], bt["blocks"], bt["shard_bytes"]
+    assert ec.shard_size(B, k) == S
+    d = fill(codec, 0, n, B, k, S)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    codec.synchronize()
+    for smp in bt["samples"]:
+        b = smp["block"]
+        assert _sha(host(d[b])) == smp["data_sha256"], (name, b)
+        assert _sha(host(p[b])) == smp["parity_sha256"], (name, b)
+    for e in bt["erasures"]:
+        s, l = ec.erasures(SEED, 0, n, k, m, e)
+        sd, ld = dev(s), dev(l)
+        surv = empty(n, k * S)
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        out = empty(n, e * S)
+        codec.rebuild(k, m, sd, surv, ld, out)
+        codec.synchronize()
+        for smp in bt["samples"]:
+            b = smp["block"]
+            r = [x for x in smp["rebuild"] if x["e"] == e][0]
+            assert list(s[b]) == r["surv"] and list(l[b]) == r["lost"], (name, b, e)
+            assert _sha(host(out[b])) == r["out_sha256"], (name, b, e)
+        del surv, out
+    del d, p
+    torch.cuda.empty_cache()

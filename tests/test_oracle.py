@@ -2,11 +2,12 @@
 the independent numpy restatement, and codec properties."""
 import hashlib
 import itertools
+import os
 
 import numpy as np
 import pytest
 
-from conftest import SEED
+from conftest import ROOT, SEED
 
 # ISO/IEC 18004 (QR code) antilog table for x^8+x^4+x^3+x^2+1, first 30 values.
 QR_EXP = [1, 2, 4, 8, 16, 32, 64, 128, 29, 58, 116, 232, 205, 135, 19, 38, 76, 152, 45, 90,
@@ -185,3 +186,27 @@ def test_two_restatements_agree(O, k, m, B, seed, block, data):
     assert np.array_equal(O.decode_matrix(k, m, s[0], l[0]), N.decode_matrix(k, m, s[0], l[0]))
     got = O.rebuild(k, m, S, s, O.gather(k, m, S, d, par, s), l)
     assert np.array_equal(got, O.gather(k, m, S, d, par, l))
+
+
+def test_c_oracle_matches_headline_digests(O):
+    """The C oracle (rs_oracle.c) reproduces the numpy restatement's digests
+    for the headline shapes' sample blocks (tests/golden/rs_headline.json):
+    fill, parity and every rebuilt shard."""
+    import hashlib
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "rs_headline.json")) as f:
+        hl = json.load(f)
+    sha = lambda x: hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()  # noqa: E731
+    for bt in hl["batches"]:
+        k, m, B, S = bt["k"], bt["m"], bt["block_bytes"], bt["shard_bytes"]
+        for smp in bt["samples"]:
+            b = smp["block"]
+            data = O.fill_blocks(SEED, b, 1, B, k, S)
+            assert sha(data) == smp["data_sha256"], (bt["name"], b)
+            par = O.encode(k, m, S, data)
+            assert sha(par) == smp["parity_sha256"], (bt["name"], b)
+            for r in smp["rebuild"]:
+                s, l = O.erasures(SEED, b, 1, k, m, r["e"])
+                assert list(s[0]) == r["surv"] and list(l[0]) == r["lost"]
+                out = O.rebuild(k, m, S, s, O.gather(k, m, S, data, par, s), l)
+                assert sha(out) == r["out_sha256"], (bt["name"], b, r["e"])
