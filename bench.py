@@ -166,7 +166,8 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
     """Small-block rebuild: 4 KiB blocks (~4 GiB of payload), 4 random
     erasures per block, so every block has its own decode rows and a
     256-column tile spans up to 17 blocks.  Encode of the same blocks is
-    timed beside it (same process, same clocks)."""
+    timed beside it (same process, same clocks), and so is the repair case
+    of one pattern for every block (memo_ec_rebuild_uniform)."""
     res = {}
     for (k, m) in [(10, 4), (16, 4)]:
         B, n, e = 4096, 1 << 20, 4
@@ -188,14 +189,29 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
         codec.synchronize()
         ms = float(np.mean(rkms))
         alg = (k + e) * S * n
+        ok = bool(torch.equal(out, want))
+        # the repair case: one lost node, every block the same pattern
+        # (memo_ec_rebuild_uniform), here block 0's
+        su, lu = s_idx[0], l_idx[0]
+        sdu = torch.from_numpy(np.ascontiguousarray(np.tile(su, (n, 1)))).cuda()
+        ldu = torch.from_numpy(np.ascontiguousarray(np.tile(lu, (n, 1)))).cuda()
+        codec.gather_shards(k, m, S, n, d, p, sdu, surv)
+        codec.gather_shards(k, m, S, n, d, p, ldu, want)
+        _, (ukms,), _ = timed_steps(torch, [lambda: codec.rebuild_uniform(k, m, su, surv, lu, out)],
+                                    steps, warmup, settle_ms, None, stream)
+        codec.synchronize()
+        ums = float(np.mean(ukms))
         res["RS(%d,%d)" % (k, m)] = {
             "blocks": n, "block_bytes": B, "shard_bytes": S, "erasures": e,
             "step_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
             "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
             "encode_frac_same_blocks": round((k + m) * S * n / (float(np.mean(ekms)) * 1e-3) / 1e9
                                              / PEAK_HBM_GBS, 4),
-            "bit_exact": bool(torch.equal(out, want))}
-        del d, p, surv, out, want, sd, ld
+            "bit_exact": ok,
+            "uniform_pattern": {"step_ms": round(ums, 4),
+                                "frac": round(alg / (ums * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                                "bit_exact": bool(torch.equal(out, want))}}
+        del d, p, surv, out, want, sd, ld, sdu, ldu
     return res
 
 

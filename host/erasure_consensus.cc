@@ -191,6 +191,18 @@ void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
   ++rebuild_calls_;
 }
 
+void Codec::rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
+                            const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out) {
+  split(n, [&](size_t d, size_t b0, size_t cnt) {
+    auto* c = acquire(d);
+    const int rc = memo_ec_rebuild_uniform(c, k, m, S, cnt, surv_idx, surv + b0 * k * S, lost_idx, e,
+                                           out + b0 * e * S, MEMO_EC_HOST);
+    release(d, c);
+    return rc;
+  }, "rebuild_uniform");
+  ++uniform_calls_;
+}
+
 // ---------------------------------------------------------- shard format
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc) {
   uint64_t c = crc ^ 0xFFFFFFFFu;
@@ -833,16 +845,38 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   std::vector<Gathered> g(n);
   pool_.parallel_for(imm.size(), [&](size_t t) { g[imm[t]] = collect(addresses[imm[t]], false); });
   tm.lap("gather");
-  std::map<std::pair<int, size_t>, std::vector<size_t>> groups;
+  // degraded blocks by (S bucket, erasure pattern); patterns shared by at
+  // least uniform_min blocks (a node down) take the uniform rebuild, the
+  // rest group by (S bucket, e) for the per-block rebuild
+  std::map<std::pair<int, std::vector<uint8_t>>, std::vector<size_t>> by_pat;
   std::vector<size_t> direct;
   for (size_t i : imm) {
-    if (g[i].err)
+    if (g[i].err) {
       errs[i] = g[i].err;
-    else if (g[i].lost.empty())
+    } else if (g[i].lost.empty()) {
       direct.push_back(i);
-    else
-      groups[{size_bucket(g[i].h.shard_size), g[i].lost.size()}].push_back(i);
+    } else {
+      std::vector<uint8_t> pat;
+      for (auto& sh : g[i].shards) pat.push_back((uint8_t)sh.first);
+      pat.insert(pat.end(), g[i].lost.begin(), g[i].lost.end());
+      by_pat[{size_bucket(g[i].h.shard_size), std::move(pat)}].push_back(i);
+    }
   }
+  struct FGroup {
+    int e;
+    bool uniform;
+    std::vector<uint8_t> pat;
+    std::vector<size_t> ids;
+  };
+  std::vector<FGroup> groups;
+  std::map<std::pair<int, size_t>, std::vector<size_t>> rest;
+  for (auto& bp : by_pat) {
+    const int e = (int)(bp.first.second.size() - (size_t)k);
+    if ((int)bp.second.size() >= o_.uniform_min) groups.push_back({e, true, bp.first.second, bp.second});
+    else rest[{bp.first.first, (size_t)e}].insert(rest[{bp.first.first, (size_t)e}].end(),
+                                                  bp.second.begin(), bp.second.end());
+  }
+  for (auto& r : rest) groups.push_back({(int)r.first.second, false, {}, r.second});
   auto finish = [&](size_t i, const uint8_t* rebuilt, size_t stride) {
     try {
       blocks[i] = assemble(addresses[i], g[i], rebuilt, stride);
@@ -853,8 +887,8 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   pool_.parallel_for(direct.size(), [&](size_t t) { finish(direct[t], nullptr, 0); });
   tm.lap("assemble_direct");
   for (auto& grp : groups) {
-    const int e = (int)grp.first.second;
-    auto& ids = grp.second;
+    const int e = grp.e;
+    auto& ids = grp.ids;
     for (size_t b0 = 0; b0 < ids.size(); b0 += o_.batch_max) {
       const size_t nb = std::min<size_t>(o_.batch_max, ids.size() - b0);
       size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
@@ -873,7 +907,11 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
         std::copy(x.lost.begin(), x.lost.end(), lidx.begin() + bi * e);
       });
       tm.lap("copy_in");
-      codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data());
+      if (grp.uniform)
+        codec_.rebuild_uniform(k, m, S, nb, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
+                               out.data());
+      else
+        codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data());
       tm.lap("rebuild");
       decoded_ += nb;
       pool_.parallel_for(nb, [&](size_t bi) { finish(ids[b0 + bi], out.data() + bi * e * S, S); });
@@ -973,19 +1011,41 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       }
       work.push_back(&x);
     }
-    // batches of blocks with the same (S bucket, e): one GPU rebuild call each
-    std::map<std::pair<int, size_t>, std::vector<Todo*>> groups;
-    for (auto* x : work) groups[{size_bucket(memo_ec_shard_size(x->pl.B, k)), x->lost.size()}].push_back(x);
-    for (auto& g : groups) {
-      const int e = (int)g.first.second;
-      for (size_t b0 = 0; b0 < g.second.size(); b0 += o_.batch_max) {
-        const size_t n = std::min<size_t>(o_.batch_max, g.second.size() - b0);
+    // Batches of blocks with the same (S bucket, e): one GPU rebuild call
+    // each; blocks that also share their erasure pattern -- the repair of
+    // one lost node -- take the uniform rebuild (shared tables, encode speed).
+    struct Group {
+      int e;
+      bool uniform;
+      std::vector<uint8_t> pat;  // survivors (k) || lost (e), uniform groups
+      std::vector<Todo*> items;
+    };
+    std::map<std::pair<int, std::vector<uint8_t>>, std::vector<Todo*>> by_pat;
+    for (auto* x : work) {
+      std::vector<uint8_t> pat;
+      for (int s = 0; s < k; ++s) pat.push_back((uint8_t)x->surv[s].first);
+      for (int i : x->lost) pat.push_back((uint8_t)i);
+      by_pat[{size_bucket(memo_ec_shard_size(x->pl.B, k)), std::move(pat)}].push_back(x);
+    }
+    std::vector<Group> gs;
+    std::map<std::pair<int, size_t>, std::vector<Todo*>> rest;
+    for (auto& bp : by_pat) {
+      const int e = (int)(bp.first.second.size() - (size_t)k);
+      if ((int)bp.second.size() >= o_.uniform_min) gs.push_back({e, true, bp.first.second, bp.second});
+      else
+        for (auto* x : bp.second) rest[{bp.first.first, (size_t)e}].push_back(x);
+    }
+    for (auto& r : rest) gs.push_back({(int)r.first.second, false, {}, r.second});
+    for (auto& grp : gs) {
+      const int e = grp.e;
+      for (size_t b0 = 0; b0 < grp.items.size(); b0 += o_.batch_max) {
+        const size_t n = std::min<size_t>(o_.batch_max, grp.items.size() - b0);
         size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
-        for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(g.second[b0 + bi]->pl.B, k));
+        for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(grp.items[b0 + bi]->pl.B, k));
         std::vector<uint8_t> sidx(n * k), lidx(n * e);
         Scratch surv(n * k * S), out(n * e * S);
         pool_.parallel_for(n, [&](size_t bi) {
-          Todo& x = *g.second[b0 + bi];
+          Todo& x = *grp.items[b0 + bi];
           const size_t Sb = memo_ec_shard_size(x.pl.B, k);
           for (int s = 0; s < k; ++s) {
             uint8_t* slot = surv.data() + (bi * k + s) * S;
@@ -997,14 +1057,18 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           x.surv.clear();
           x.surv.shrink_to_fit();
         });
-        codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
+        if (grp.uniform)
+          codec_.rebuild_uniform(k, m, S, n, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
+                                 out.data());
+        else
+          codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
         ++rep.codec_calls;
         std::vector<int> placed(n, 0);
         // place each rebuilt shard on a reachable node holding none of the
         // block's other shards (Overlay::allocate order); the stale copy on
         // a reachable old holder is dropped
         pool_.parallel_for(n, [&](size_t bi) {
-          Todo& x = *g.second[b0 + bi];
+          Todo& x = *grp.items[b0 + bi];
           std::set<Address> taken;
           for (int i = 0; i < total; ++i)
             if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
@@ -1040,7 +1104,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           }
         });
         for (size_t bi = 0; bi < n; ++bi) {
-          Todo& x = *g.second[b0 + bi];
+          Todo& x = *grp.items[b0 + bi];
           bool removed = false;
           {
             std::unique_lock<std::shared_mutex> lk(index_mu_);

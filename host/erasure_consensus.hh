@@ -50,8 +50,13 @@ class Codec {
   void encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity);
   void rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx, const uint8_t* surv,
                const uint8_t* lost_idx, int e, uint8_t* out);
+  // One erasure pattern for all n blocks (memo_ec_rebuild_uniform):
+  // surv_idx has k entries, lost_idx e.
+  void rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
+                       const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out);
   uint64_t encode_calls() const { return encode_calls_; }
   uint64_t rebuild_calls() const { return rebuild_calls_; }
+  uint64_t uniform_calls() const { return uniform_calls_; }
   size_t devices() const { return dev_.size(); }
 
  private:
@@ -69,7 +74,7 @@ class Codec {
   std::vector<memo_ec_ctx*> all_;
   std::vector<Dev> dev_;
   std::atomic<size_t> rr_{0};
-  std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0};
+  std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0}, uniform_calls_{0};
 };
 
 // ---------------------------------------------------------- shard format
@@ -131,6 +136,10 @@ struct ErasureOptions {
   int batch_max = 256;         // blocks per GPU encode / rebuild call
   int batch_window_us = 200;   // how long the batcher waits for company
   int threads = 16;            // peer fan-out (memo's background pool is <= 16)
+  // Blocks of one batch that share an erasure pattern (the repair of one
+  // lost node) go to the uniform rebuild, at encode speed, once at least
+  // this many share it; the rest to the per-block rebuild.
+  int uniform_min = 4;
   // A node that disappears is evicted -- its shards rebuilt elsewhere --
   // after this long unless it comes back ("eviction-delay", Paxos.cc:985-1009,
   // default 10 min, Paxos.hxx:35).  < 0: never automatically.

@@ -124,6 +124,22 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
                           const uint8_t *lost_idx, int e, uint8_t *out,
                           int where);
 
+/* Rebuild with ONE erasure pattern for the whole batch: every block lost the
+ * shards lost_idx[0..e) and is rebuilt from the survivors surv_idx[0..k)
+ * (host pointers: k and e bytes), surv n x k x S in surv_idx order, out
+ * n x e x S.  This is the repair of one lost node, where every block that
+ * node held shard i of shares a pattern (Paxos::LocalPeer::_disappeared_evict,
+ * src/memo/model/doughnut/consensus/Paxos.cc:1012-1087): the decode rows are
+ * formed once on the host and their product tables are shared by all
+ * blocks, as the encode's parity rows are, so the call runs at encode
+ * speed.  An invalid pattern (duplicate or out-of-range index) returns
+ * MEMO_EC_ESINGULAR before anything is enqueued.  `where` as for
+ * memo_ec_rebuild_batch (surv/out memory only). */
+int memo_ec_rebuild_uniform(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
+                            const uint8_t *surv_idx, const uint8_t *surv,
+                            const uint8_t *lost_idx, int e, uint8_t *out,
+                            int where);
+
 /* Per-block decode rows (n x e x k bytes, device): row r of block b holds the
  * coefficients of lost_idx[b][r] over the survivors in surv_idx[b] order,
  * i.e. C[lost] * inv(C[surv]) -- computed in closed form (one lane per block,

@@ -46,7 +46,15 @@ struct memo_ec_ctx {
     int k, m;
     uint32_t* dev;
   };
-  std::vector<Lw0Entry> lw0_tabs;  // cached LW0 tables per (k, m) (fused rebuild)
+  std::vector<Lw0Entry> lw0_tabs;  // cached LW0 tables per (k, m) (decode kernels)
+  struct PatEntry {
+    int k, m, R, kpad;
+    std::vector<uint8_t> key;  // surv_idx (k) || lost_idx (e)
+    uint32_t* dev;
+    uint64_t used;
+  };
+  std::vector<PatEntry> pat_tabs;  // cached uniform-rebuild table images
+  uint64_t pat_clock = 0;
   // host pipeline: device slots and pinned bounce buffers
   uint8_t* d_slot[3] = {nullptr, nullptr, nullptr};
   size_t slot_cap = 0;
@@ -555,6 +563,143 @@ int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, D
   return MEMO_EC_OK;
 }
 
+// A host-memory call of one multiply-accumulate over n blocks of in_b bytes
+// in and out_b bytes out (encode, uniform rebuild): `run(src, dst, cnt, st)`
+// enqueues the kernels for cnt blocks of device- or pinned-memory src/dst.
+// Small calls run zero-copy on pinned memory; larger ones through the
+// 3-stage copy pipeline.
+template <class Run>
+int host_mac(memo_ec_ctx* c, size_t n, size_t in_b, size_t out_b, const uint8_t* data,
+             uint8_t* out, bool pinned, Run run) {
+  if (n * (in_b + out_b) <= zc_max_bytes()) {
+    // Small call: the kernel reads the blocks from, and writes its output
+    // to, pinned host memory over PCIe -- no DMA copies to wait for.
+    if (int rc = ensure_slots(c, 0, pinned ? 0 : n * (in_b + out_b))) return rc;
+    const uint8_t* src = data;
+    uint8_t* dst = out;
+    if (!pinned) {
+      par_memcpy(c->h_slot[0], data, n * in_b);
+      src = c->h_slot[0];
+      dst = c->h_slot[0] + n * in_b;
+    }
+    if (int rc = run(src, dst, n, c->sk)) return rc;
+    HIPCHK(hipStreamSynchronize(c->sk));
+    if (!pinned) par_memcpy(out, dst, n * out_b);
+    return MEMO_EC_OK;
+  }
+  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
+  nb = std::min(nb, n);
+  if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
+  // slot layout (device and pageable bounce): [in nb*in_b | out nb*out_b]
+  return run_pipeline(
+      c, n, nb,
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
+        const uint8_t* src = data + b0 * in_b;
+        if (!pinned) {
+          par_memcpy(c->h_slot[s], src, cnt * in_b);
+          src = c->h_slot[s];
+        }
+        return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, st));
+      },
+      [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
+        return run(c->d_slot[s], c->d_slot[s] + nb * in_b, cnt, st);
+      },
+      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
+        uint8_t* dst = pinned ? out + b0 * out_b : c->h_slot[s] + nb * in_b;
+        return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + nb * in_b, cnt * out_b,
+                                     hipMemcpyDeviceToHost, st));
+      },
+      [&](int s, size_t b0, size_t cnt) {
+        if (!pinned) par_memcpy(out + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
+      });
+}
+
+// Decode rows of one erasure pattern on the host: row r = C[lost_r] *
+// inv(C[surv]) by Gauss-Jordan over GF(2^8) (k <= 64: microseconds).  False
+// for an invalid pattern (index >= k+m, duplicate survivors).
+bool host_decode_rows(int k, int m, const uint8_t* sidx, const uint8_t* lidx, int e, uint8_t* rows) {
+  const uint8_t* lg = host_gf_log();
+  const uint8_t* ex = host_gf_exp();
+  auto mul = [&](uint32_t a, uint32_t b) -> uint32_t { return (a && b) ? ex[lg[a] + lg[b]] : 0u; };
+  auto inv = [&](uint32_t a) -> uint32_t { return ex[255 - lg[a]]; };
+  const int nt = k + m;
+  std::vector<uint8_t> gen((size_t)nt * k);
+  memo_ec_generator(k, m, gen.data());
+  std::vector<int> seen(nt, 0);
+  for (int t = 0; t < k; ++t) {
+    if (sidx[t] >= nt || seen[sidx[t]]++) return false;
+  }
+  for (int r = 0; r < e; ++r)
+    if (lidx[r] >= nt) return false;
+  // A = C[surv] (k x k) | I, reduced to I | inv(A)
+  std::vector<uint8_t> A((size_t)k * 2 * k, 0);
+  for (int t = 0; t < k; ++t) {
+    std::memcpy(&A[(size_t)t * 2 * k], &gen[(size_t)sidx[t] * k], k);
+    A[(size_t)t * 2 * k + k + t] = 1;
+  }
+  for (int c = 0; c < k; ++c) {
+    int p = c;
+    while (p < k && !A[(size_t)p * 2 * k + c]) ++p;
+    if (p == k) return false;  // cannot happen for a Cauchy code
+    if (p != c)
+      for (int j = 0; j < 2 * k; ++j) std::swap(A[(size_t)p * 2 * k + j], A[(size_t)c * 2 * k + j]);
+    const uint32_t iv = inv(A[(size_t)c * 2 * k + c]);
+    for (int j = 0; j < 2 * k; ++j) A[(size_t)c * 2 * k + j] = (uint8_t)mul(A[(size_t)c * 2 * k + j], iv);
+    for (int r = 0; r < k; ++r) {
+      const uint32_t f = A[(size_t)r * 2 * k + c];
+      if (r == c || !f) continue;
+      for (int j = 0; j < 2 * k; ++j) A[(size_t)r * 2 * k + j] ^= (uint8_t)mul(f, A[(size_t)c * 2 * k + j]);
+    }
+  }
+  for (int r = 0; r < e; ++r)
+    for (int t = 0; t < k; ++t) {
+      uint32_t acc = 0;
+      for (int j = 0; j < k; ++j) acc ^= mul(gen[(size_t)lidx[r] * k + j], A[(size_t)j * 2 * k + k + t]);
+      rows[(size_t)r * k + t] = (uint8_t)acc;
+    }
+  return true;
+}
+
+// Cached device table image of one erasure pattern's decode rows (uniform
+// rebuild).  Repairs repeat a few patterns (one per shard index a lost node
+// held), so images are kept, least recently used evicted past 64.
+int pattern_tables(memo_ec_ctx* ctx, int k, int m, const uint8_t* sidx, const uint8_t* lidx, int e,
+                   int R, int KC, const uint32_t** out) {
+  const int kpad = (int)kpad_of((uint32_t)k, KC);
+  std::vector<uint8_t> key(sidx, sidx + k);
+  key.insert(key.end(), lidx, lidx + e);
+  ++ctx->pat_clock;
+  for (auto& p : ctx->pat_tabs)
+    if (p.k == k && p.m == m && p.R == R && p.kpad == kpad && p.key == key) {
+      p.used = ctx->pat_clock;
+      *out = p.dev;
+      return MEMO_EC_OK;
+    }
+  std::vector<uint8_t> rows((size_t)e * k);
+  if (!host_decode_rows(k, m, sidx, lidx, e, rows.data())) return MEMO_EC_ESINGULAR;
+  std::vector<uint32_t> img((size_t)R * kpad * 8);
+  table_image_host(rows.data(), (uint32_t)e, (uint32_t)k, (uint32_t)R, (uint32_t)kpad, img.data());
+  if (ctx->pat_tabs.size() >= 64) {
+    // the evicted image may still be read by enqueued work on this ctx
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (int rc = sync_pipeline(ctx)) return rc;
+    auto lru = std::min_element(ctx->pat_tabs.begin(), ctx->pat_tabs.end(),
+                                [](const auto& a, const auto& b) { return a.used < b.used; });
+    HIPCHK(hipFree(lru->dev));
+    ctx->pat_tabs.erase(lru);
+  }
+  uint32_t* dev = nullptr;
+  HIPCHK(hipMalloc(&dev, img.size() * 4));
+  hipError_t err = hipMemcpy(dev, img.data(), img.size() * 4, hipMemcpyHostToDevice);
+  if (err != hipSuccess) {
+    (void)hipFree(dev);
+    return hip_rc(err);
+  }
+  ctx->pat_tabs.push_back({k, m, R, kpad, std::move(key), dev, ctx->pat_clock});
+  *out = dev;
+  return MEMO_EC_OK;
+}
+
 int take_deferred(memo_ec_ctx* ctx) {
   uint32_t st = 0;
   HIPCHK(hipMemcpy(&st, ctx->d_status, sizeof st, hipMemcpyDeviceToHost));
@@ -667,6 +812,7 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
   if (c->d_tabs) (void)hipFree(c->d_tabs);
   for (auto& e : c->enc_tabs) (void)hipFree(e.dev);
   for (auto& e : c->lw0_tabs) (void)hipFree(e.dev);
+  for (auto& e : c->pat_tabs) (void)hipFree(e.dev);
   if (c->d_status) (void)hipFree(c->d_status);
   if (c->h_status) (void)hipHostFree(c->h_status);
   for (int i = 0; i < kSlots; ++i)
@@ -713,49 +859,39 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   if (where == MEMO_EC_DEVICE) return encode_device(c, k, m, S, n, data, parity, c->stream);
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
 
-  const size_t in_b = (size_t)k * S, out_b = (size_t)m * S;
-  const bool pinned = where == MEMO_EC_HOST_PINNED;
-  if (n * (in_b + out_b) <= zc_max_bytes()) {
-    // Small call: the kernel reads the blocks from, and writes the parity
-    // to, pinned host memory over PCIe -- no DMA copies to wait for.
-    if (int rc = ensure_slots(c, 0, pinned ? 0 : n * (in_b + out_b))) return rc;
-    const uint8_t* src = data;
-    uint8_t* dst = parity;
-    if (!pinned) {
-      par_memcpy(c->h_slot[0], data, n * in_b);
-      src = c->h_slot[0];
-      dst = c->h_slot[0] + n * in_b;
+  return host_mac(c, n, (size_t)k * S, (size_t)m * S, data, parity,
+                  where == MEMO_EC_HOST_PINNED,
+                  [&](const uint8_t* src, uint8_t* dst, size_t cnt, hipStream_t st) {
+                    return encode_device(c, k, m, S, cnt, src, dst, st);
+                  });
+}
+
+int memo_ec_rebuild_uniform(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
+                            const uint8_t* surv_idx, const uint8_t* surv, const uint8_t* lost_idx,
+                            int e, uint8_t* out, int where) {
+  if (!c) return MEMO_EC_EINVAL;
+  if (int rc = check_km(k, m)) return rc;
+  if (e < 0 || e > m) return MEMO_EC_EINVAL;
+  if (e == 0 || n == 0) return MEMO_EC_OK;
+  if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  const int R = mac_rbound(e), KC = mac_kchunk(k, R);
+  const uint32_t* tab = nullptr;
+  if (int rc = pattern_tables(c, k, m, surv_idx, lost_idx, e, R, KC, &tab)) return rc;
+  auto run = [&](const uint8_t* src, uint8_t* dst, size_t cnt, hipStream_t st) -> int {
+    const size_t step = max_blocks_per_launch(S);
+    for (size_t b0 = 0; b0 < cnt; b0 += step) {
+      const size_t bc = std::min(step, cnt - b0);
+      std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, bc, src + b0 * (size_t)k * S,
+                                           (uint64_t)k * S, S, dst + b0 * (size_t)e * S,
+                                           (uint64_t)e * S, S, tab, 0, KC, R)};
+      if (int rc = launch_plans(plans, st)) return rc;
     }
-    if (int rc = encode_device(c, k, m, S, n, src, dst, c->sk)) return rc;
-    HIPCHK(hipStreamSynchronize(c->sk));
-    if (!pinned) par_memcpy(parity, dst, n * out_b);
     return MEMO_EC_OK;
-  }
-  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
-  nb = std::min(nb, n);
-  if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
-  // slot layout (device and pageable bounce): [data nb*in_b | parity nb*out_b]
-  return run_pipeline(
-      c, n, nb,
-      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
-        const uint8_t* src = data + b0 * in_b;
-        if (!pinned) {
-          par_memcpy(c->h_slot[s], src, cnt * in_b);
-          src = c->h_slot[s];
-        }
-        return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, st));
-      },
-      [&](int s, size_t, size_t cnt, hipStream_t st) -> int {
-        return encode_device(c, k, m, S, cnt, c->d_slot[s], c->d_slot[s] + nb * in_b, st);
-      },
-      [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
-        uint8_t* dst = pinned ? parity + b0 * out_b : c->h_slot[s] + nb * in_b;
-        return hip_rc(hipMemcpyAsync(dst, c->d_slot[s] + nb * in_b, cnt * out_b,
-                                     hipMemcpyDeviceToHost, st));
-      },
-      [&](int s, size_t b0, size_t cnt) {
-        if (!pinned) par_memcpy(parity + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
-      });
+  };
+  if (where == MEMO_EC_DEVICE) return run(surv, out, n, c->stream);
+  if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
+  return host_mac(c, n, (size_t)k * S, (size_t)e * S, surv, out, where == MEMO_EC_HOST_PINNED, run);
 }
 
 int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* surv_idx,

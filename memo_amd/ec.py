@@ -48,7 +48,7 @@ _LIB = None
 EXPORTS = [
     "memo_ec_ctx_create", "memo_ec_ctx_destroy", "memo_ec_set_stream", "memo_ec_get_stream",
     "memo_ec_synchronize", "memo_ec_shard_size", "memo_ec_generator", "memo_ec_encode_batch",
-    "memo_ec_rebuild_batch", "memo_ec_decode_rows", "memo_ec_encode_segments",
+    "memo_ec_rebuild_batch", "memo_ec_rebuild_uniform", "memo_ec_decode_rows", "memo_ec_encode_segments",
     "memo_ec_sha256_batch", "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards",
     "memo_ec_strerror",
     "memo_ec_version", "memo_ec_device_count",
@@ -74,6 +74,8 @@ def _lib():
         L.memo_ec_encode_batch.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p, c_int]
         L.memo_ec_rebuild_batch.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
                                             _u8p, c_int, _u8p, c_int]
+        L.memo_ec_rebuild_uniform.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
+                                              _u8p, c_int, _u8p, c_int]
         L.memo_ec_decode_rows.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _u8p, _u8p, c_int, _u8p]
         L.memo_ec_encode_segments.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(Segment)]
         L.memo_ec_sha256_batch.argtypes = [ctypes.c_void_p, _sz, _u8p, _sz, _sz, _u8p, _sz,
@@ -235,6 +237,22 @@ class Codec:
             where = HOST_PINNED if sw == ow == HOST_PINNED else HOST
         _check(_lib().memo_ec_rebuild_batch(self._ctx, k, m, S, n, ip, sp, lp, e, op, where),
                "rebuild")
+        return out
+
+    def rebuild_uniform(self, k, m, surv_idx, surv, lost_idx, out, S=None, n=None):
+        """out (n x e x S) <- surv (n x k x S) with ONE erasure pattern for the
+        whole batch: surv_idx (k) and lost_idx (e) are host sequences."""
+        sp, sw = _ptr(surv)
+        op, ow = _ptr(out)
+        if (sw == DEVICE) != (ow == DEVICE):
+            raise ValueError("surv and out must both be device or both host buffers")
+        si = np.ascontiguousarray(np.asarray(surv_idx, dtype=np.uint8).reshape(-1))
+        li = np.ascontiguousarray(np.asarray(lost_idx, dtype=np.uint8).reshape(-1))
+        if S is None:
+            n, S = _infer_nS(surv, k)
+        where = DEVICE if sw == DEVICE else (HOST_PINNED if sw == ow == HOST_PINNED else HOST)
+        _check(_lib().memo_ec_rebuild_uniform(self._ctx, k, m, S, n, si.ctypes.data, sp,
+                                              li.ctypes.data, len(li), op, where), "rebuild_uniform")
         return out
 
     def decode_rows(self, k, m, surv_idx, lost_idx, rows):

@@ -724,3 +724,61 @@ def test_headline_batches_vs_numpy_digests(codec, name, rebuild_path):
         del surv, out
     del d, p
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (10, 4), (16, 4), (6, 3), (12, 4), (20, 8), (64, 16)])
+def test_rebuild_uniform_vs_oracle(codec, O, k, m):
+    """One erasure pattern for a whole batch (the repair of one lost node):
+    device-resident and host-memory calls (zero-copy and pipeline), lost
+    shards that are data, parity or survivors (unit rows), against the
+    true shards."""
+    import torch
+    rng = np.random.default_rng(k * 31 + m)
+    for B, n in [(4096, 300), (100000, 5), (1 << 20, 70)]:
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 50, n, B, k, S)
+        par = O.encode(k, m, S, data, threads=4)
+        for e in sorted({1, m}):
+            perm = rng.permutation(k + m)
+            surv = np.sort(perm[:k]).astype(np.uint8) if e % 2 else perm[:k].astype(np.uint8)
+            lost = rng.permutation(k + m)[:e].astype(np.uint8)
+            s_all = np.tile(surv, (n, 1))
+            want = O.gather(k, m, S, data, par, np.tile(lost, (n, 1)))
+            sv = O.gather(k, m, S, data, par, s_all)
+            out = empty(n, e * S)
+            codec.rebuild_uniform(k, m, surv, dev(sv), lost, out)
+            codec.synchronize()
+            assert np.array_equal(host(out), want), (k, m, B, e, "device")
+            ho = np.zeros((n, e * S), np.uint8)
+            codec.rebuild_uniform(k, m, surv, sv, lost, ho)
+            assert np.array_equal(ho, want), (k, m, B, e, "host")
+            po = torch.zeros((n, e * S), dtype=torch.uint8).pin_memory()
+            codec.rebuild_uniform(k, m, surv, torch.from_numpy(sv).pin_memory(), lost, po)
+            assert np.array_equal(po.numpy(), want), (k, m, B, e, "pinned")
+
+
+def test_rebuild_uniform_invalid_and_cache(codec, O):
+    """An invalid pattern is refused before anything is enqueued; more
+    distinct patterns than the ctx caches (64) are each rebuilt right."""
+    from memo_amd import ec
+    k, m, B, n = 10, 4, 5000, 7
+    S = O.shard_size(B, k)
+    sv = empty(n, k * S).zero_()
+    out = empty(n, S)
+    for surv, lost in ([[0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [9]], [[0, 1, 2, 3, 4, 5, 6, 7, 8, 14], [9]],
+                       [list(range(10)), [14]]):
+        with pytest.raises(ec.MemoECError) as ei:
+            codec.rebuild_uniform(k, m, surv, sv, lost, out)
+        assert ei.value.code == -4
+    codec.synchronize()
+    data = O.fill_blocks(SEED, 1, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    rng = np.random.default_rng(5)
+    for i in range(80):
+        perm = rng.permutation(k + m)
+        surv, lost = perm[:k].astype(np.uint8), perm[k:k + 2].astype(np.uint8)
+        o = empty(n, 2 * S)
+        codec.rebuild_uniform(k, m, surv, dev(O.gather(k, m, S, data, par, np.tile(surv, (n, 1)))),
+                              lost, o)
+        codec.synchronize()
+        assert np.array_equal(host(o), O.gather(k, m, S, data, par, np.tile(lost, (n, 1)))), i
