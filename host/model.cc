@@ -5,6 +5,8 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <filesystem>
+#include <cstdio>
 #include <random>
 #include <sstream>
 
@@ -184,6 +186,116 @@ std::vector<Key> MemorySilo::_list() {
   std::lock_guard<std::mutex> g(mu_);
   std::vector<Key> out;
   for (auto& kv : blocks_) out.push_back(kv.first);
+  return out;
+}
+
+// ------------------------------------------------------ filesystem silo
+namespace {
+namespace fs = std::filesystem;
+std::string hex_of(const uint8_t* p, size_t n) {
+  static const char* d = "0123456789abcdef";
+  std::string s;
+  for (size_t i = 0; i < n; ++i) {
+    s += d[p[i] >> 4];
+    s += d[p[i] & 15];
+  }
+  return s;
+}
+bool key_of(const std::string& name, Key& out) {
+  if (name.size() != 64) return false;
+  uint8_t v[32];
+  for (int i = 0; i < 32; ++i) {
+    auto nib = [](char c) -> int {
+      return c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10 : -1;
+    };
+    const int hi = nib(name[2 * i]), lo = nib(name[2 * i + 1]);
+    if (hi < 0 || lo < 0) return false;
+    v[i] = (uint8_t)(hi << 4 | lo);
+  }
+  out = Address(v, 0, false);
+  return true;
+}
+}  // namespace
+
+FilesystemSilo::FilesystemSilo(std::string root, int64_t capacity)
+    : Silo(capacity), root_(std::move(root)) {
+  fs::create_directories(root_);
+  int64_t used = 0;
+  for (auto& dir : fs::directory_iterator(root_))
+    if (dir.is_directory())
+      for (auto& f : fs::directory_iterator(dir.path())) {
+        Key k;
+        if (f.is_regular_file() && key_of(f.path().filename().string(), k)) used += (int64_t)f.file_size();
+      }
+  usage_ = used;
+}
+
+std::string FilesystemSilo::path(const Key& k, bool make_dir) const {
+  const std::string dir = root_ + "/" + hex_of(k.value.data(), 1);
+  if (make_dir) fs::create_directories(dir);
+  return dir + "/" + hex_of(k.value.data(), 32);
+}
+
+bool FilesystemSilo::_try_get(const Key& k, Buffer& out) const {
+  std::FILE* f = std::fopen(path(k, false).c_str(), "rb");
+  if (!f) return false;
+  std::fseek(f, 0, SEEK_END);
+  const long n = std::ftell(f);
+  std::fseek(f, 0, SEEK_SET);
+  out.resize(n > 0 ? (size_t)n : 0);
+  const size_t got = n > 0 ? std::fread(out.data(), 1, (size_t)n, f) : 0;
+  std::fclose(f);
+  if (got != out.size()) throw Error("filesystem silo: short read " + k.hex());
+  return true;
+}
+
+Buffer FilesystemSilo::_get(const Key& k) const {
+  Buffer out;
+  if (!_try_get(k, out)) throw silo::MissingKey("missing key " + k.hex());
+  return out;
+}
+
+bool FilesystemSilo::_contains(const Key& k) const { return fs::exists(path(k, false)); }
+
+int FilesystemSilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
+  const std::string p = path(k, true);
+  std::lock_guard<std::mutex> g(mu_);
+  std::error_code ec;
+  const bool exists = fs::exists(p);
+  const int64_t old = exists ? (int64_t)fs::file_size(p, ec) : 0;
+  if (!exists && !insert) throw silo::MissingKey("missing key " + k.hex());
+  if (exists && !update) throw silo::Collision("key exists " + k.hex());
+  const std::string tmp = p + ".tmp";
+  std::FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) throw Error("filesystem silo: cannot write " + tmp);
+  const size_t put = v.empty() ? 0 : std::fwrite(v.data(), 1, v.size(), f);
+  const bool ok = std::fclose(f) == 0 && put == v.size();
+  if (!ok) {
+    fs::remove(tmp, ec);
+    throw Error("filesystem silo: short write " + k.hex());
+  }
+  fs::rename(tmp, p);
+  return (int)((int64_t)v.size() - old);
+}
+
+int FilesystemSilo::_erase(const Key& k) {
+  const std::string p = path(k, false);
+  std::lock_guard<std::mutex> g(mu_);
+  std::error_code ec;
+  if (!fs::exists(p)) throw silo::MissingKey("missing key " + k.hex());
+  const int64_t old = (int64_t)fs::file_size(p, ec);
+  fs::remove(p);
+  return -(int)old;
+}
+
+std::vector<Key> FilesystemSilo::_list() {
+  std::vector<Key> out;
+  for (auto& dir : fs::directory_iterator(root_))
+    if (dir.is_directory())
+      for (auto& f : fs::directory_iterator(dir.path())) {
+        Key k;
+        if (f.is_regular_file() && key_of(f.path().filename().string(), k)) out.push_back(k);
+      }
   return out;
 }
 

@@ -181,6 +181,30 @@ class MemorySilo : public Silo {
   std::map<Key, std::shared_ptr<const Buffer>> blocks_;
 };
 
+// silo::Filesystem (src/memo/silo/Filesystem.cc:27-147): one file per key,
+// named by the key's hex, in a subdirectory named by its first byte; usage
+// recovered from the files present at construction.  Writes go to a temp
+// file renamed into place, so a crash leaves the old value or the new one.
+class FilesystemSilo : public Silo {
+ public:
+  explicit FilesystemSilo(std::string root, int64_t capacity = -1);
+  std::string type() const override { return "filesystem"; }
+  const std::string& root() const { return root_; }
+
+ protected:
+  Buffer _get(const Key& k) const override;
+  bool _try_get(const Key& k, Buffer& out) const override;
+  bool _contains(const Key& k) const override;
+  int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
+  int _erase(const Key& k) override;
+  std::vector<Key> _list() override;
+
+ private:
+  std::string path(const Key& k, bool make_dir) const;
+  std::string root_;
+  mutable std::mutex mu_;  // serialises writers of one key with its readers
+};
+
 // ------------------------------------------------------------ peers/overlay
 // A storage node: doughnut::Local with its silo (Local.cc:180-257) as seen
 // through Peer::store/fetch/remove (doughnut/Peer.hh:19-89).  `up` models

@@ -8,6 +8,7 @@
 #include <mutex>
 #include <cstdio>
 #include <cstring>
+#include <filesystem>
 #include <random>
 #include <set>
 #include <thread>
@@ -148,6 +149,46 @@ TEST(silo_memory_contract, false) {
   s.erase(k1);
   CHECK_THROW(s.get(k1), silo::MissingKey);
   CHECK(s.list().empty());
+}
+
+std::string temp_dir(const char* tag) {
+  char tmpl[256];
+  std::snprintf(tmpl, sizeof tmpl, "/tmp/memo_ec_%s_XXXXXX", tag);
+  const char* d = mkdtemp(tmpl);
+  if (!d) throw Error("mkdtemp failed");
+  return d;
+}
+
+// tests/storage.cc:15-45 on silo::Filesystem (Filesystem.cc:27-147): the
+// same contract, and what was stored survives reopening the directory
+// (usage recovered from the files).
+TEST(silo_filesystem_contract, false) {
+  const std::string root = temp_dir("silo");
+  Key k1 = Address::random(flags::immutable_block), k2 = Address::random(flags::immutable_block);
+  {
+    FilesystemSilo s(root);
+    s.set(k1, bytes("the grey"));
+    CHECK(s.get(k1) == bytes("the grey"));
+    s.set(k1, bytes("the white"), false, true);
+    CHECK(s.get(k1) == bytes("the white"));
+    CHECK_THROW(s.set(k1, Buffer()), silo::Collision);
+    CHECK_THROW(s.get(k2), silo::MissingKey);
+    CHECK_THROW(s.set(k2, Buffer(), false, true), silo::MissingKey);
+    CHECK_THROW(s.erase(k2), silo::MissingKey);
+    s.set(k2, Buffer(1000, 7));
+    CHECK(s.usage() == 9 + 1000);
+  }
+  {
+    FilesystemSilo s(root);  // reopened
+    CHECK(s.usage() == 9 + 1000);
+    auto keys = s.list();
+    CHECK(keys.size() == 2);
+    CHECK(s.get(k1) == bytes("the white"));
+    s.erase(k1);
+    CHECK_THROW(s.get(k1), silo::MissingKey);
+    CHECK(s.usage() == 1000);
+  }
+  std::filesystem::remove_all(root);
 }
 
 // tests/storage.cc:47-84: capacity.
@@ -713,6 +754,58 @@ TEST(evict_one_node_uses_uniform_rebuild, true) {
   CHECK(uniform >= 1);
   CHECK(rep.codec_calls < held);
   for (auto& b : blocks) CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// A real restart: every node's shards in a filesystem silo; the whole
+// in-process network (overlay, nodes, consensus) is torn down and rebuilt
+// over the same directories.  The fresh consensus rebuilds its indices from
+// the shard headers on disk, reads every block, and, after one node's disk
+// is lost and the node evicted, repairs exactly that node's blocks.
+TEST(restart_from_filesystem_silos, true) {
+  const std::string root = temp_dir("net");
+  const int N = 16;
+  std::vector<Block> blocks;
+  for (int i = 0; i < 40; ++i) blocks.push_back(make_chb(random_bytes(3000 + 4099 * i, 700 + i)));
+  ErasureOptions o;
+  o.k = 10;
+  o.m = 4;
+  o.eviction_delay_ms = -1;
+  auto node_id = [](int i) {
+    uint8_t id[32] = {0};
+    id[0] = (uint8_t)(i + 1);
+    id[1] = 0x46;
+    return Address(id, 0, false);
+  };
+  {
+    Overlay ov;
+    for (int i = 0; i < N; ++i)
+      ov.add_node(node_id(i), std::make_unique<FilesystemSilo>(root + "/n" + std::to_string(i)));
+    ErasureConsensus ec(std::make_unique<ReplicationConsensus>(ov, 3), ov, o);
+    ec.store_many(blocks);
+  }
+  Overlay ov;
+  std::vector<std::shared_ptr<Node>> nodes;
+  for (int i = 0; i < N; ++i)
+    nodes.push_back(ov.add_node(node_id(i), std::make_unique<FilesystemSilo>(root + "/n" + std::to_string(i))));
+  auto ec = std::make_unique<ErasureConsensus>(std::make_unique<ReplicationConsensus>(ov, 3), ov, o);
+  CHECK(from_json(ec->stats())["blocks"] == "40");
+  for (auto& b : blocks) CHECK(ec->fetch(b.address)->data == b.data);
+  // node 3 loses its disk and is evicted
+  const size_t held = ec->node_blocks(nodes[3]->id);
+  CHECK(held > 0);
+  nodes[3]->up = false;
+  std::filesystem::remove_all(root + "/n3");
+  auto rep = ec->evict(nodes[3]->id);
+  CHECK(rep.blocks_repaired == held && rep.unrecoverable == 0);
+  int down = 0;
+  for (auto& n : nodes)
+    if (n != nodes[3] && down < 4) {
+      n->up = false;
+      ++down;
+    }
+  for (auto& b : blocks) CHECK(ec->fetch(b.address)->data == b.data);
+  ec.reset();
+  std::filesystem::remove_all(root);
 }
 
 // Redundancy JSON (Consensus::redundancy, Paxos.cc:2218-2225 shape).
