@@ -247,6 +247,29 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   return w;
 }
 
+ShardHeader decode_shard_header(const uint8_t* w, size_t n) {
+  if (n < ShardHeader::kSize || std::memcmp(w, "MECS", 4) != 0) throw ValidationFailed("shard: bad magic");
+  ShardHeader h;
+  h.version = w[4];
+  h.k = w[5];
+  h.m = w[6];
+  h.index = w[7];
+  std::memcpy(&h.block_size, w + 8, 8);
+  std::memcpy(&h.shard_size, w + 16, 8);
+  h.address = Address(w + 24, 0, false);
+  uint32_t sl;
+  std::memcpy(&sl, w + 56, 4);
+  if (h.version != ShardHeader::kVersion) throw ValidationFailed("shard: unknown version");
+  if (sl > 32) throw ValidationFailed("shard: bad salt length");
+  h.salt.assign(w + 60, w + 60 + sl);
+  h.owner = Address(w + 92, 0, false);
+  std::memcpy(&h.crc, w + kCrcAt, 4);
+  if (h.k < 1 || h.index >= h.k + h.m) throw ValidationFailed("shard: bad geometry");
+  if (h.shard_size != memo_ec_shard_size(h.block_size, h.k))
+    throw ValidationFailed("shard: size does not match block size");
+  return h;
+}
+
 ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
   if (w.size() < ShardHeader::kSize || std::memcmp(w.data(), "MECS", 4) != 0)
     throw ValidationFailed("shard: bad magic");
@@ -1186,10 +1209,10 @@ size_t ErasureConsensus::rescan() {
     auto& nd = nodes[ni];
     if (!nd->up || nd->evicted) return;
     for (const Key& key : nd->silo->list()) {
-      Buffer w;
-      if (!nd->silo->try_get(key, w)) continue;
+      Buffer w;  // the header only: payloads are checked when read
+      if (!nd->silo->try_get_prefix(key, ShardHeader::kSize, w)) continue;
       try {
-        ShardHeader h = decode_shard(w, nullptr);
+        ShardHeader h = decode_shard_header(w.data(), w.size());
         // this code's shards only, under their own key
         if (h.k != o_.k || h.m != o_.m || shard_key(h.address, h.index) != key) continue;
         per[ni].push_back({std::move(h), nd->id});

@@ -107,6 +107,10 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
 // Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
 // payload length, CRC32C over header and payload); throws ValidationFailed.
 ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
+// The header alone (the first kSize bytes): magic, version and geometry are
+// checked, the checksum cannot be (it covers the payload).  Index rescans
+// use it; fetch and repair validate whole shards.
+ShardHeader decode_shard_header(const uint8_t* wire, size_t n);
 // Silo key of shard `index` of block `address`.
 Key shard_key(const Address& address, int index);
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);

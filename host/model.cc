@@ -121,6 +121,12 @@ bool Silo::_try_get(const Key& k, Buffer& out) const {
   }
 }
 
+bool Silo::_try_get_prefix(const Key& k, size_t n, Buffer& out) const {
+  if (!_try_get(k, out)) return false;
+  if (out.size() > n) out.resize(n);
+  return true;
+}
+
 bool Silo::_contains(const Key& k) const {
   Buffer tmp;
   return _try_get(k, tmp);
@@ -249,6 +255,15 @@ bool FilesystemSilo::_try_get(const Key& k, Buffer& out) const {
   return true;
 }
 
+bool FilesystemSilo::_try_get_prefix(const Key& k, size_t n, Buffer& out) const {
+  std::FILE* f = std::fopen(path(k, false).c_str(), "rb");
+  if (!f) return false;
+  out.resize(n);
+  out.resize(std::fread(out.data(), 1, n, f));
+  std::fclose(f);
+  return true;
+}
+
 Buffer FilesystemSilo::_get(const Key& k) const {
   Buffer out;
   if (!_try_get(k, out)) throw silo::MissingKey("missing key " + k.hex());
@@ -335,8 +350,7 @@ std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo>
     nodes_.push_back(n);
     by_id_[n->id] = n;
   }
-  for (auto& h : handlers())
-    if (h.discovered) h.discovered(id);
+  notify([](const Handlers& h) -> const NodeEvent& { return h.discovered; }, id);
   return n;
 }
 
@@ -355,10 +369,8 @@ void Overlay::set_up(const Address& id, bool up) {
   auto n = node(id);
   if (!n) throw Error("overlay: unknown node " + id.hex());
   if (n->up.exchange(up) == up) return;
-  for (auto& h : handlers()) {
-    const NodeEvent& f = up ? h.appeared : h.disappeared;
-    if (f) f(id);
-  }
+  if (up) notify([](const Handlers& h) -> const NodeEvent& { return h.appeared; }, id);
+  else notify([](const Handlers& h) -> const NodeEvent& { return h.disappeared; }, id);
 }
 
 std::shared_ptr<Node> Overlay::node(const Address& id) const {

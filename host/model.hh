@@ -140,6 +140,9 @@ class Silo {
   Buffer get(const Key& k) const { return _get(k); }
   // get() without the MissingKey exception: false when absent.
   bool try_get(const Key& k, Buffer& out) const { return _try_get(k, out); }
+  // The first n bytes of the value (all of it if shorter); false when
+  // absent.  Index rescans read shard headers only.
+  bool try_get_prefix(const Key& k, size_t n, Buffer& out) const { return _try_get_prefix(k, n, out); }
   bool contains(const Key& k) const { return _contains(k); }
   // insert: accept a new key; update: accept an existing key.
   int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
@@ -153,6 +156,7 @@ class Silo {
   virtual Buffer _get(const Key& k) const = 0;
   virtual bool _try_get(const Key& k, Buffer& out) const;  // default: _get + catch
   virtual bool _contains(const Key& k) const;                // default: _try_get
+  virtual bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const;  // default: _try_get
   virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
   virtual int _erase(const Key& k) = 0;
   virtual std::vector<Key> _list() = 0;
@@ -195,6 +199,7 @@ class FilesystemSilo : public Silo {
   Buffer _get(const Key& k) const override;
   bool _try_get(const Key& k, Buffer& out) const override;
   bool _contains(const Key& k) const override;
+  bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const override;
   int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
   int _erase(const Key& k) override;
   std::vector<Key> _list() override;
@@ -263,14 +268,18 @@ class Overlay {
   mutable std::shared_mutex mu_;
   std::vector<std::shared_ptr<Node>> nodes_;
   std::unordered_map<Address, std::shared_ptr<Node>, AddressHash> by_id_;
+  // Handlers run under hmu_: once unsubscribe() returns, none of that
+  // subscriber's handlers is running or will run.
   std::mutex hmu_;
   std::map<int, Handlers> handlers_;
   int next_token_ = 0;
-  std::vector<Handlers> handlers() {
+  template <class F>
+  void notify(F pick, const Address& id) {
     std::lock_guard<std::mutex> g(hmu_);
-    std::vector<Handlers> out;
-    for (auto& kv : handlers_) out.push_back(kv.second);
-    return out;
+    for (auto& kv : handlers_) {
+      const NodeEvent& f = pick(kv.second);
+      if (f) f(id);
+    }
   }
 };
 

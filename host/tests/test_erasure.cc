@@ -221,6 +221,8 @@ TEST(shard_format_round_trip_and_validation, false) {
   CHECK(d.address == h.address && d.salt == h.salt && d.owner == h.owner);
   CHECK(d.same_block(h));
   CHECK(std::memcmp(p, payload.data(), h.shard_size) == 0);
+  ShardHeader hd = decode_shard_header(w.data(), ShardHeader::kSize);  // header bytes only
+  CHECK(hd.same_block(h) && hd.index == 12 && hd.crc == d.crc);
   Buffer bad = w;
   bad[ShardHeader::kSize + 5] ^= 1;  // payload bit flip
   CHECK_THROW(decode_shard(bad, nullptr), ValidationFailed);
