@@ -1198,17 +1198,46 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
 // so a block's survivor set is one 32-bit mask; its m non-survivors are
 // extracted once into registers (ctz), every loop is unrolled at compile
 // time (rows r < e by uniform predicates), the rows are packed into dwords
-// before they are staged in LDS (e*K/4 dword stores instead of e*K byte
-// stores), and LW0 comes from the host's per-code table.  Same results as
-// decode_coef_kernel (tests/test_gpu_parity.py); about half its VALU work.
+// before they are staged in LDS, and LW0 comes from the host's per-code
+// table.  The coefficient of (lost l, survivor s) costs one XOR, two LDS
+// lookups and one v_add3_u32:
+//   row_l[t] = EX[lw_t + llam_l + NLG[l ^ s_t]]
+// with NLG = 255 - log (so no subtraction), and log sums kept unreduced
+// but folded once ((x & 255) + (x >> 8) == x mod 255, 2 ops): lw_t <= 271,
+// llam_l = 510 - fold(...) in [239, 510], so the index stays below 1040 and
+// EX is 2^(i mod 255) over 1280 entries.  Duplicate and out-of-range
+// indices are found from the mask and an OR of all indices (no per-index
+// tests); a faulty block's rows are zeroed once at the end.  Same results
+// as decode_coef_kernel (tests/test_gpu_parity.py).
+struct DecTables {
+  uint8_t lg[256];    // log
+  uint8_t nlg[256];   // 255 - log (nlg[0]: 0, never used for a non-unit row)
+  uint8_t ex[1280];   // 2^(i mod 255)
+};
+constexpr DecTables make_dec_tables() {
+  DecTables t{};
+  const GfTables g = make_gf();
+  for (int i = 0; i < 256; ++i) {
+    t.lg[i] = g.log[i];
+    t.nlg[i] = i ? (uint8_t)(255 - g.log[i]) : 0;
+  }
+  for (int i = 0; i < 1280; ++i) t.ex[i] = g.exp[i % 255];
+  return t;
+}
+__constant__ DecTables kDec = make_dec_tables();
+constexpr int kDecDwords = sizeof(DecTables) / 4;
+
+__device__ __forceinline__ uint32_t fold255(uint32_t x) { return (x & 0xFFu) + (x >> 8); }
+
 template <int K>
 __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
   static_assert(K <= 16, "one 32-bit survivor mask: K + MEMO_EC_MAX_M <= 32");
-  __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
+  __shared__ __attribute__((aligned(16))) uint32_t s_tab[kDecDwords];
   __shared__ uint32_t s_lw0[32];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch
-  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
-  const uint8_t* ex = lg + 256;
+  const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_tab);
+  const uint8_t* nlg = lg + 256;
+  const uint8_t* ex = lg + 512;
   const uint8_t* lw0 = reinterpret_cast<const uint8_t*>(s_lw0);
   const uint32_t m = a.m, e = a.e, nt = K + a.m;
   const uint32_t tid = threadIdx.x;
@@ -1252,25 +1281,31 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
     for (int r = 0; r < MEMO_EC_MAX_M; ++r) lv[r] = (live && (uint32_t)r < e) ? a.lost_idx[b * e + r] : 0u;
   }
   {
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&kGf);
-    for (uint32_t i = tid; i < kGfDwords; i += 256) s_gf[i] = src[i];
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&kDec);
+    for (uint32_t i = tid; i < kDecDwords; i += 256) s_tab[i] = src[i];
     if (tid < 32) s_lw0[tid] = a.lw0[tid];
   }
   __syncthreads();
   const uint32_t ek = e * K;
   uint32_t* out = reinterpret_cast<uint32_t*>(s_out + tid * a.pitch);
   if (live) {
-    // survivor set: range and duplicates
-    uint32_t mask = 0;
-    bool bad = false;
+    // survivor set: a duplicate leaves fewer than K bits, an index >= nt a
+    // bit at or past nt (or past 31: caught by the OR of all indices)
+    uint32_t mask = 0, any = 0;
 #pragma unroll
     for (int t = 0; t < K; ++t) {
-      const uint32_t v = sv[t], bit = 1u << (v & 31);
-      bad |= v >= nt || (mask & bit) != 0;
-      mask |= bit;
+      mask |= 1u << (sv[t] & 31);
+      any |= sv[t];
     }
+    uint32_t lany = 0;
+#pragma unroll
+    for (int r = 0; r < MEMO_EC_MAX_M; ++r)
+      if ((uint32_t)r < e) lany |= lv[r] >= nt ? 1u : 0u;
+    const uint32_t valid = nt >= 32 ? ~0u : (1u << nt) - 1u;
+    const bool bad = (uint32_t)__popc(mask) != (uint32_t)K || (mask & ~valid) != 0 || (any >> 5) != 0 ||
+                     lany != 0;
     // the m non-survivors, in registers
-    uint32_t comp = ~mask & (nt >= 32 ? ~0u : (1u << nt) - 1u);
+    uint32_t comp = ~mask & valid;
     uint32_t cl[MEMO_EC_MAX_M];
 #pragma unroll
     for (int q = 0; q < MEMO_EC_MAX_M; ++q) {
@@ -1280,38 +1315,46 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
         comp &= comp - 1;
       }
     }
-    // log W_t = LW0(s_t) + sum_c log(s_t ^ c)
+    // log W_t = LW0(s_t) + sum_c log(s_t ^ c), folded once (<= 271)
     uint32_t lw[K];
 #pragma unroll
     for (int t = 0; t < K; ++t) lw[t] = lw0[sv[t] & 31];
 #pragma unroll
-    for (int q = 0; q < MEMO_EC_MAX_M; ++q)
-      if ((uint32_t)q < m) {
+    for (int q = 0; q < MEMO_EC_MAX_M; q += 2) {
+      if ((uint32_t)q + 1 < m) {
+#pragma unroll
+        for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]] + lg[sv[t] ^ cl[q + 1]];
+      } else if ((uint32_t)q < m) {
 #pragma unroll
         for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]];
       }
+    }
 #pragma unroll
-    for (int t = 0; t < K; ++t) lw[t] = mod255(lw[t]) + 255u;
+    for (int t = 0; t < K; ++t) lw[t] = fold255(lw[t]);
     // rows, packed 4 bytes per dword
     uint32_t word = 0;
 #pragma unroll
     for (int r = 0; r < MEMO_EC_MAX_M; ++r) {
       if ((uint32_t)r < e) {
-        const uint32_t l = lv[r];
-        bad |= l >= nt;
+        const uint32_t l = lv[r] & 0xFFu;
         const bool unit = (mask >> (l & 31)) & 1u;
         uint32_t acc = lw0[l & 31];
 #pragma unroll
         for (int q = 0; q < MEMO_EC_MAX_M; ++q)
           if ((uint32_t)q < m) acc += lg[l ^ cl[q]];  // c == l adds log[0] = 0
-        const uint32_t llam = 255u - mod255(acc);   // log Lam_l, in 1..255
+        const uint32_t llam = 510u - fold255(acc);   // == -log(Lam_l) mod 255, in [239, 510]
+        uint32_t v[K];
+        if (!unit) {
+#pragma unroll
+          for (int t = 0; t < K; ++t) v[t] = ex[lw[t] + llam + nlg[l ^ sv[t]]];  // < 1040
+        } else {  // l itself survived: a unit row (rare: callers name lost shards)
+#pragma unroll
+          for (int t = 0; t < K; ++t) v[t] = sv[t] == l ? 1u : 0u;
+        }
 #pragma unroll
         for (int t = 0; t < K; ++t) {
-          // lw + llam - log(l ^ s_t) < 765
-          uint32_t v = unit ? (sv[t] == l ? 1u : 0u) : ex[lw[t] + llam - lg[l ^ sv[t]]];
-          v = bad ? 0u : v;
           const int q = r * K + t;  // compile-time byte position
-          word |= v << (8 * (q & 3));
+          word |= v[t] << (8 * (q & 3));
           if ((q & 3) == 3) {
             out[q >> 2] = word;
             word = 0;
