@@ -1780,18 +1780,20 @@ hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   pw |= 1u;
   a.pitch = 256u * pw * 4 <= 64 * 1024 ? pw * 4 : 0u;
   const size_t lds = a.pitch ? 256u * a.pitch : 0;
-  // exact-k kernels for the common codes (MEMO_EC_DECODE_EXACT=0: off; read
+  // exact-k kernels for the common codes, k in {2, 3, 4, 6, 8, 10, 12, 14,
+  // 16} (MEMO_EC_DECODE_EXACT=0: off; read
   // per call, for A/B runs and tests)
   const char* ex_env = std::getenv("MEMO_EC_DECODE_EXACT");
   const bool exact = !ex_env || std::atoi(ex_env) != 0;
   if (exact && a.pitch && a.lw0 && a.k + a.m <= 32) {
     switch (a.k) {
-      case 4: hipLaunchKernelGGL(decode_rows_k_kernel<4>, dim3(grid), dim3(256), lds, st, a);
-        return hipGetLastError();
-      case 10: hipLaunchKernelGGL(decode_rows_k_kernel<10>, dim3(grid), dim3(256), lds, st, a);
-        return hipGetLastError();
-      case 16: hipLaunchKernelGGL(decode_rows_k_kernel<16>, dim3(grid), dim3(256), lds, st, a);
-        return hipGetLastError();
+#define MEMO_EC_DK(x)                                                                    \
+  case x:                                                                                \
+    hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), lds, st, a);      \
+    return hipGetLastError();
+      MEMO_EC_DK(2) MEMO_EC_DK(3) MEMO_EC_DK(4) MEMO_EC_DK(6) MEMO_EC_DK(8) MEMO_EC_DK(10)
+      MEMO_EC_DK(12) MEMO_EC_DK(14) MEMO_EC_DK(16)
+#undef MEMO_EC_DK
       default: break;
     }
   }

@@ -156,8 +156,8 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
     assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost))
 
 
-@pytest.mark.parametrize("k,m", [(1, 1), (3, 2), (4, 2), (7, 5), (10, 4), (16, 4), (20, 8),
-                                 (33, 12), (64, 16)])
+@pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 2), (4, 2), (6, 3), (7, 5), (8, 8), (10, 4),
+                                 (12, 4), (14, 2), (16, 4), (16, 16), (20, 8), (33, 12), (64, 16)])
 @pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_generic"])
 def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
     """Closed-form decode rows against the oracle's Gauss-Jordan rows
@@ -166,7 +166,8 @@ def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
     blocks (several workgroups).  Both kernels: column-per-lane
     (decode_coef_wide_kernel, small batches) and one lane per block
     (forced by MEMO_EC_DECODE_WIDE_MAX=0: decode_rows_k_kernel for k in
-    {4, 10, 16}, decode_coef_kernel otherwise or with MEMO_EC_DECODE_EXACT=0)."""
+    {2, 3, 4, 6, 8, 10, 12, 14, 16}, decode_coef_kernel otherwise or with
+    MEMO_EC_DECODE_EXACT=0)."""
     if kernel != "wide":
         monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
     if kernel == "per_block_generic":
