@@ -467,38 +467,70 @@ ShardHeader ErasureConsensus::header_of(const Address& a, const Placement& pl, i
   return h;
 }
 
-void ErasureConsensus::set_placement_locked(const Address& a, Placement pl) {
+std::vector<Address> ErasureConsensus::swap_placement_locked(const Address& a, Placement pl) {
+  std::vector<Address> old;
   auto it = index_.find(a);
-  if (it != index_.end())
-    for (auto& h : it->second.holder) {
-      if (!h) continue;
-      auto nb = node_blocks_.find(h);
-      if (nb == node_blocks_.end()) continue;
-      nb->second.erase(a);
-      if (nb->second.empty()) node_blocks_.erase(nb);
-    }
-  for (auto& h : pl.holder)
-    if (h) node_blocks_[h].insert(a);
-  index_[a] = std::move(pl);
-}
-
-void ErasureConsensus::erase_placement_locked(const Address& a) {
-  auto it = index_.find(a);
-  if (it == index_.end()) return;
-  for (auto& h : it->second.holder) {
-    if (!h) continue;
-    auto nb = node_blocks_.find(h);
-    if (nb == node_blocks_.end()) continue;
-    nb->second.erase(a);
-    if (nb->second.empty()) node_blocks_.erase(nb);
+  if (it != index_.end()) {
+    old = std::move(it->second.holder);
+    it->second = std::move(pl);
+  } else {
+    index_.emplace(a, std::move(pl));
   }
-  index_.erase(it);
+  return old;
 }
 
-size_t ErasureConsensus::node_blocks(const Address& node) const {
-  std::shared_lock<std::shared_mutex> g(index_mu_);
-  auto it = node_blocks_.find(node);
-  return it == node_blocks_.end() ? 0 : it->second.size();
+std::vector<Address> ErasureConsensus::erase_placement_locked(const Address& a) {
+  std::vector<Address> old;
+  auto it = index_.find(a);
+  if (it == index_.end()) return old;
+  old = std::move(it->second.holder);
+  index_.erase(it);
+  return old;
+}
+
+size_t ErasureConsensus::node_blocks(const Address& node) const { return nodes_.count(node); }
+
+// ------------------------------------------------------------ node index
+NodeIndex::Stripe& NodeIndex::stripe(const Address& node) const {
+  return st_[AddressHash()(node) % kStripes];
+}
+
+void NodeIndex::update(const Address& block, const std::vector<Address>& old_h,
+                       const std::vector<Address>& new_h) {
+  auto has = [](const std::vector<Address>& v, const Address& x) {
+    return std::find(v.begin(), v.end(), x) != v.end();
+  };
+  for (size_t i = 0; i < old_h.size(); ++i) {
+    const Address& h = old_h[i];
+    if (!h || has(new_h, h) || std::find(old_h.begin(), old_h.begin() + i, h) != old_h.begin() + i)
+      continue;
+    Stripe& s = stripe(h);
+    std::lock_guard<std::mutex> g(s.mu);
+    auto it = s.m.find(h);
+    if (it == s.m.end()) continue;
+    it->second.erase(block);
+    if (it->second.empty()) s.m.erase(it);
+  }
+  for (const Address& h : new_h) {
+    if (!h || has(old_h, h)) continue;
+    Stripe& s = stripe(h);
+    std::lock_guard<std::mutex> g(s.mu);
+    s.m[h].insert(block);
+  }
+}
+
+std::vector<Address> NodeIndex::blocks(const Address& node) const {
+  Stripe& s = stripe(node);
+  std::lock_guard<std::mutex> g(s.mu);
+  auto it = s.m.find(node);
+  return it == s.m.end() ? std::vector<Address>() : std::vector<Address>(it->second.begin(), it->second.end());
+}
+
+size_t NodeIndex::count(const Address& node) const {
+  Stripe& s = stripe(node);
+  std::lock_guard<std::mutex> g(s.mu);
+  auto it = s.m.find(node);
+  return it == s.m.end() ? 0 : it->second.size();
 }
 
 void ErasureConsensus::on_rebalanced(std::function<void(const Address&)> f) {
@@ -593,10 +625,13 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
       pl.holder[i] = owners[i]->id;
       ++reached;
     }
+  const std::vector<Address> holders = pl.holder;
+  std::vector<Address> old;
   {
     std::unique_lock<std::shared_mutex> g(index_mu_);
-    set_placement_locked(b.address, std::move(pl));
+    old = swap_placement_locked(b.address, std::move(pl));
   }
+  nodes_.update(b.address, old, holders);
   if (reached < o_.k)
     throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
                       std::to_string(o_.k));
@@ -895,7 +930,9 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   std::map<std::pair<int, size_t>, std::vector<size_t>> rest;
   for (auto& bp : by_pat) {
     const int e = (int)(bp.first.second.size() - (size_t)k);
-    if ((int)bp.second.size() >= o_.uniform_min) groups.push_back({e, true, bp.first.second, bp.second});
+    const size_t bytes = bp.second.size() * (size_t)k * ((size_t)64 << bp.first.first);
+    if ((int)bp.second.size() >= o_.uniform_min && bytes >= o_.uniform_min_bytes)
+      groups.push_back({e, true, bp.first.second, bp.second});
     else rest[{bp.first.first, (size_t)e}].insert(rest[{bp.first.first, (size_t)e}].end(),
                                                   bp.second.begin(), bp.second.end());
   }
@@ -949,8 +986,12 @@ void ErasureConsensus::_remove(const Address& a) {
   {
     // forget the block first: a repair running concurrently will not
     // re-place it (evict_removed_blocks, tests/doughnut.cc:1693-1719)
-    std::unique_lock<std::shared_mutex> g(index_mu_);
-    erase_placement_locked(a);
+    std::vector<Address> old;
+    {
+      std::unique_lock<std::shared_mutex> g(index_mu_);
+      old = erase_placement_locked(a);
+    }
+    nodes_.update(a, old, {});
   }
   for (auto& nd : overlay_.lookup(a, (int)overlay_.size()))
     for (int i = 0; i < o_.k + o_.m; ++i) {
@@ -975,10 +1016,26 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     std::vector<std::pair<int, Buffer>> surv;    // k validated survivor shards (wire)
     bool skip = false;
   };
-  // Chunks of blocks: the survivors of one chunk are held in memory at once.
-  const size_t chunk = (size_t)std::max(64, o_.batch_max) * std::max<size_t>(1, codec_.devices());
-  for (size_t c0 = 0; c0 < blocks.size(); c0 += chunk) {
-    const size_t cn = std::min(chunk, blocks.size() - c0);
+  // Chunks of blocks whose survivors are held in memory at once: up to
+  // kChunkBytes of shards (by the recorded block sizes), so that small blocks
+  // still fill whole GPU batches per (size, e) group.
+  constexpr size_t kChunkBytes = 512u << 20;
+  std::vector<size_t> cuts{0};
+  {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    size_t acc = 0;
+    for (size_t i = 0; i < blocks.size(); ++i) {
+      auto it = index_.find(blocks[i]);
+      acc += (size_t)k * memo_ec_shard_size(it == index_.end() ? 0 : it->second.B, k);
+      if (acc >= kChunkBytes && i + 1 - cuts.back() >= (size_t)o_.batch_max) {
+        cuts.push_back(i + 1);
+        acc = 0;
+      }
+    }
+    if (cuts.back() != blocks.size()) cuts.push_back(blocks.size());
+  }
+  for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+    const size_t c0 = cuts[ci], cn = cuts[ci + 1] - c0;
     std::vector<Todo> todo(cn);
     // Scan: a shard is lost when its holder is gone (null, evicted, down
     // with include_down), lacks it, or holds a copy that fails validation
@@ -1054,7 +1111,9 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     std::map<std::pair<int, size_t>, std::vector<Todo*>> rest;
     for (auto& bp : by_pat) {
       const int e = (int)(bp.first.second.size() - (size_t)k);
-      if ((int)bp.second.size() >= o_.uniform_min) gs.push_back({e, true, bp.first.second, bp.second});
+      const size_t bytes = bp.second.size() * (size_t)k * ((size_t)64 << bp.first.first);
+      if ((int)bp.second.size() >= o_.uniform_min && bytes >= o_.uniform_min_bytes)
+        gs.push_back({e, true, bp.first.second, bp.second});
       else
         for (auto* x : bp.second) rest[{bp.first.first, (size_t)e}].push_back(x);
     }
@@ -1129,11 +1188,13 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         for (size_t bi = 0; bi < n; ++bi) {
           Todo& x = *grp.items[b0 + bi];
           bool removed = false;
+          std::vector<Address> old;
           {
             std::unique_lock<std::shared_mutex> lk(index_mu_);
-            if (index_.count(x.a)) set_placement_locked(x.a, x.pl);
+            if (index_.count(x.a)) old = swap_placement_locked(x.a, x.pl);
             else removed = true;
           }
+          if (!removed) nodes_.update(x.a, old, x.pl.holder);
           if (removed) {  // removed while being repaired: drop the new shards
             for (int i : x.lost)
               if (x.pl.holder[i])
@@ -1173,12 +1234,7 @@ ErasureConsensus::RepairReport ErasureConsensus::evict(const Address& node) {
     std::lock_guard<std::mutex> g(mmu_);
     evict_at_.erase(node);
   }
-  std::vector<Address> blocks;
-  {
-    std::shared_lock<std::shared_mutex> g(index_mu_);
-    auto it = node_blocks_.find(node);
-    if (it != node_blocks_.end()) blocks.assign(it->second.begin(), it->second.end());
-  }
+  const std::vector<Address> blocks = nodes_.blocks(node);
   ++evictions_;
   return repair_blocks(blocks, false);
 }
@@ -1241,8 +1297,16 @@ size_t ErasureConsensus::rescan() {
       Address& h = found[s.h.address].holder[s.h.index];
       if (!h) h = s.node;
     }
-  std::unique_lock<std::shared_mutex> g(index_mu_);
-  for (auto& kv : found) set_placement_locked(kv.first, std::move(kv.second));
+  std::vector<std::pair<Address, std::vector<Address>>> diff;  // (block, old holders)
+  std::vector<std::vector<Address>> neu;
+  {
+    std::unique_lock<std::shared_mutex> g(index_mu_);
+    for (auto& kv : found) {
+      neu.push_back(kv.second.holder);
+      diff.emplace_back(kv.first, swap_placement_locked(kv.first, std::move(kv.second)));
+    }
+  }
+  for (size_t i = 0; i < diff.size(); ++i) nodes_.update(diff[i].first, diff[i].second, neu[i]);
   return found.size();
 }
 

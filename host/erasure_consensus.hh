@@ -133,6 +133,30 @@ class ThreadPool {
   bool stop_ = false;
 };
 
+// ------------------------------------------------------------ node index
+// Node -> blocks it holds a shard of (Paxos::_node_blocks by_node,
+// Paxos.hh:403-434), striped by node so that concurrent placements (the
+// store pool) do not serialise on one lock.  Updated after the placement
+// index: an eviction that races a placement may miss that block, which the
+// full repair() scan still finds.
+class NodeIndex {
+ public:
+  // old holders -> new holders of `block` (null addresses ignored)
+  void update(const Address& block, const std::vector<Address>& old_h,
+              const std::vector<Address>& new_h);
+  std::vector<Address> blocks(const Address& node) const;
+  size_t count(const Address& node) const;
+
+ private:
+  static constexpr size_t kStripes = 32;
+  struct Stripe {
+    mutable std::mutex mu;
+    std::unordered_map<Address, std::unordered_set<Address, AddressHash>, AddressHash> m;
+  };
+  Stripe& stripe(const Address& node) const;
+  mutable std::array<Stripe, kStripes> st_;
+};
+
 // ---------------------------------------------------------------- options
 struct ErasureOptions {
   int k = 10, m = 4;
@@ -142,8 +166,11 @@ struct ErasureOptions {
   int threads = 16;            // peer fan-out (memo's background pool is <= 16)
   // Blocks of one batch that share an erasure pattern (the repair of one
   // lost node) go to the uniform rebuild, at encode speed, once at least
-  // this many share it; the rest to the per-block rebuild.
+  // uniform_min blocks and uniform_min_bytes of survivors share it (below
+  // that a separate GPU call costs more than the per-block decode it saves);
+  // the rest to the per-block rebuild.
   int uniform_min = 4;
+  size_t uniform_min_bytes = 8u << 20;
   // A node that disappears is evicted -- its shards rebuilt elsewhere --
   // after this long unless it comes back ("eviction-delay", Paxos.cc:985-1009,
   // default 10 min, Paxos.hxx:35).  < 0: never automatically.
@@ -234,9 +261,11 @@ class ErasureConsensus : public StackedConsensus {
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);
-  // index_ and node_blocks_ together (callers hold index_mu_ exclusively)
-  void set_placement_locked(const Address& a, Placement pl);
-  void erase_placement_locked(const Address& a);
+  // index_ updates under index_mu_ (held exclusively by the caller); they
+  // return the block's previous holders for the node index, which the
+  // caller updates after releasing the lock
+  std::vector<Address> swap_placement_locked(const Address& a, Placement pl);
+  std::vector<Address> erase_placement_locked(const Address& a);
   // The repair engine: rebuild and re-place the lost shards of `blocks`.
   RepairReport repair_blocks(const std::vector<Address>& blocks, bool include_down);
   // membership: overlay events -> the membership thread
@@ -249,8 +278,7 @@ class ErasureConsensus : public StackedConsensus {
   ThreadPool pool_;
   mutable std::shared_mutex index_mu_;  // readers: fetch paths; writers: place, repair, remove
   std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_quorums analogue
-  // node -> blocks it holds a shard of (Paxos::_node_blocks, Paxos.hh:403-434)
-  std::unordered_map<Address, std::unordered_set<Address, AddressHash>, AddressHash> node_blocks_;
+  NodeIndex nodes_;  // node -> blocks it holds a shard of
   std::mutex repair_mu_;  // one repair engine run at a time
   std::function<void(const Address&)> rebalanced_;
   // batcher (host C++ batching of concurrent stores into one GPU call)

@@ -739,6 +739,8 @@ TEST(evict_removed_blocks, true) {
 // (shared tables) in a few calls, not one per block.
 TEST(evict_one_node_uses_uniform_rebuild, true) {
   Net net(16, 10, 4);
+  net.o.uniform_min_bytes = 0;  // small blocks here: take every shared pattern
+  net.restart();
   std::vector<Block> blocks;
   for (int i = 0; i < 96; ++i) blocks.push_back(make_chb(random_bytes(30000 + 13 * i, 5000 + i)));
   net.ec->store_many(blocks);
