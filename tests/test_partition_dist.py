@@ -148,18 +148,22 @@ BENCH_SMALL = ["--gpus", "2", "--same-device", "--steps", "3", "--warmup", "2", 
 
 
 @pytest.mark.gpu
-def test_bench_launches_its_own_ranks():
-    """`python bench.py --gpus 2` with no external launcher starts both ranks
-    itself (both on cuda:0 here; one per GPU on a node), each encoding and
+@pytest.mark.parametrize("ranks", [2, 4])
+def test_bench_launches_its_own_ranks(ranks):
+    """`python bench.py --gpus N` with no external launcher starts the N ranks
+    itself (all on cuda:0 here; one per GPU on a node), each encoding and
     rebuilding its own 64 blocks; rank 0 prints one line."""
     import subprocess
     import sys
-    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + BENCH_SMALL,
+    args = list(BENCH_SMALL)
+    args[args.index("--gpus") + 1] = str(ranks)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     res = _bench_json(r)
-    assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 128
+    assert res["n_gpus"] == ranks and res["config"]["global_blocks"] == 64 * ranks
     assert res["value"] > 0 and res["rebuild"]["round_trip_bit_exact"]
-    assert len(res["ranks"]["per_gpu"]) == 2 and res["ranks"]["node_sum_GiBs"] > 0
+    assert [p["rank"] for p in res["ranks"]["per_gpu"]] == list(range(ranks))
+    assert res["ranks"]["node_sum_GiBs"] > 0
 
 
 @pytest.mark.gpu
