@@ -117,7 +117,7 @@ def kstats(kms, alg_bytes):
             "achieved": round(achieved, 1), "frac": round(achieved / PEAK_HBM_GBS, 4)}
 
 
-def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms):
+def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
     """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
     ~gib GiB of payload per point, one encode launch per step; then the same
     12 smaller groups as ONE memo_ec_encode_segments call (one launch per
@@ -135,9 +135,26 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms):
                                        settle_ms, None, stream)
             ms = float(np.mean(kms))
             alg = (k + m) * S * n
-            points.append({"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
-                           "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
-                           "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)})
+            pt = {"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
+                  "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
+                  "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+            if cpu:
+                # CPU baseline of the point (per C5 point): the
+                # vectorised port on 16 threads over a ~64 MiB sample of the blocks
+                from oracle import oracle as O
+                nc = max(16, min(n, (64 << 20) // B))
+                hd = O.aligned_empty((nc, k * S))
+                hd[:] = d[:nc].cpu().numpy()
+                hp = O.aligned_empty((nc, m * S))
+                th = max(1, min(host_cores(), 16))
+                _, isa = O.encode_simd(k, m, S, hd, threads=th, out=hp)
+                ok = bool(np.array_equal(hp[:2], p[:2].cpu().numpy()))
+                cv, _, _ = _rate(lambda: O.encode_simd(k, m, S, hd, threads=th, isa=isa, out=hp),
+                                 nc * B, 0.4)
+                pt["cpu_GiBs"] = round(cv, 2)
+                pt["cpu_threads"] = th
+                pt["cpu_bit_exact"] = ok
+            points.append(pt)
             del d, p
     segs, alg, pay = [], 0, 0
     for (k, m) in [(4, 2), (10, 4), (16, 4)]:
@@ -270,6 +287,19 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                      nball * B, 3.0)
     sc_all, _, _ = _rate(lambda: O.encode(k, m, S, data[:32], threads=threads), 32 * B, 2.0)
     sc_one, _, _ = _rate(lambda: O.encode(k, m, S, data[:2], threads=1), 2 * B, 1.0)
+    # the rebuild configs (C3): the same blocks, 4 random erasures each,
+    # per-block decode rows + the vectorised MAC (oracle/rs_simd.c)
+    e = min(4, m)
+    s_idx, l_idx = O.erasures(SEED, 0, nb, k, m, e)
+    surv = O.gather(k, m, S, data, par, s_idx)
+    want = O.gather(k, m, S, data, par, l_idx)
+    rout = O.aligned_empty((nb, e * S))
+    O.rebuild_simd(k, m, S, s_idx, surv, l_idx, threads=threads, isa=isa, out=rout)
+    ok_reb = bool(np.array_equal(rout, want))
+    rv, _, _ = _rate(lambda: O.rebuild_simd(k, m, S, s_idx, surv, l_idx, threads=threads, isa=isa,
+                                            out=rout), nb * B, 3.0)
+    rone, _, _ = _rate(lambda: O.rebuild_simd(k, m, S, s_idx[:16], surv[:16], l_idx[:16], threads=1,
+                                              isa=isa, out=rout[:16]), 16 * B, 1.0)
     return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": "RS(%d,%d) encode, %d x %d-byte blocks x %d passes (%.1f s), vectorised C port "
                       "(%s, streaming stores) on %d threads; all %d affinity cores %.3f GiB/s; "
@@ -279,6 +309,10 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                          threads, sc_one, nchk, ok_simd and ok_scalar),
             "isa": O.SIMD_ISA[isa], "single_core": round(one, 3),
             "all_cores": {"cores": cores, "value": round(va, 3), "blocks": nball},
+            "rebuild": {"value": round(rv, 3), "single_core": round(rone, 3), "threads": threads,
+                        "erasures": e, "bit_exact": ok_reb,
+                        "sample": "RS(%d,%d) rebuild of the same %d blocks, %d random erasures each "
+                                  "(decode rows by Gauss-Jordan + vectorised MAC)" % (k, m, nb, e)},
             "scalar_oracle": {"value": round(sc_all, 3), "single_core": round(sc_one, 3)},
             "bit_exact_vs_gpu": ok_simd and ok_scalar}
 
@@ -573,7 +607,7 @@ def main():
         if args.sweep:
             del data, par
             result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4),
-                                    args.warmup, args.settle_ms)
+                                    args.warmup, args.settle_ms, cpu=not args.no_cpu)
 
     if rank == 0:
         print(json.dumps(result), flush=True)

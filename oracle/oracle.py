@@ -49,6 +49,8 @@ def lib():
         L.memo_oracle_encode_simd_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p,
                                                  ctypes.c_int, ctypes.c_int]
         L.memo_oracle_simd_isa.argtypes = []
+        L.memo_oracle_rebuild_simd_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, u8p,
+                                                  ctypes.c_int, u8p, ctypes.c_int, ctypes.c_int]
         L.memo_oracle_rebuild.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, u8p, ctypes.c_int, u8p]
         L.memo_oracle_rebuild_mt.argtypes = [ctypes.c_int, ctypes.c_int, sz, sz, u8p, u8p, u8p,
                                              ctypes.c_int, u8p, ctypes.c_int]
@@ -153,6 +155,22 @@ def encode_simd(k, m, S, data, threads=1, isa=-1, out=None):
     if used < 0:
         raise ValueError("encode_simd rejected k=%d m=%d" % (k, m))
     return par, used
+
+
+def rebuild_simd(k, m, S, surv_idx, surv, lost_idx, threads=1, isa=-1, out=None):
+    """Vectorised CPU rebuild (rs_simd.c): per-block decode rows by the scalar
+    oracle, the MAC by GFNI/AVX-512 or AVX2.  Returns (out, isa used)."""
+    surv_idx = np.ascontiguousarray(surv_idx, dtype=np.uint8)
+    lost_idx = np.ascontiguousarray(lost_idx, dtype=np.uint8)
+    n, e = lost_idx.shape
+    surv = np.ascontiguousarray(surv, dtype=np.uint8).reshape(n, k * S)
+    if out is None:
+        out = np.zeros((n, e * S), dtype=np.uint8)
+    used = lib().memo_oracle_rebuild_simd_mt(k, m, S, n, _p(surv_idx), _p(surv), _p(lost_idx), e,
+                                             _p(out), threads, isa)
+    if used < 0:
+        raise ValueError("rebuild_simd rejected the input")
+    return out, used
 
 
 def rebuild(k, m, S, surv_idx, surv, lost_idx, threads=1):

@@ -28,6 +28,8 @@
 
 int memo_oracle_cauchy(int k, int m, uint8_t *a);
 uint8_t memo_oracle_gf_mul(uint8_t a, uint8_t b);
+int memo_oracle_decode_matrix(int k, int m, const uint8_t *surv, const uint8_t *lost, int e,
+                              uint8_t *out);
 
 enum { ISA_SCALAR = 0, ISA_AVX2 = 1, ISA_GFNI512 = 2 };
 
@@ -194,4 +196,74 @@ int memo_oracle_encode_simd_mt(int k, int m, size_t S, size_t n, const uint8_t *
     if (isa == ISA_GFNI512) sfence_all();
     free(th); free(jobs); free(C); free(aff); free(nib);
     return isa;
+}
+
+/* Rebuild with the same vectorised kernels (the CPU baseline of the rebuild
+ * configs): per block, the decode rows C[lost] * inv(C[surv]) of the scalar
+ * oracle (Gauss-Jordan), their affine matrices / nibble tables, then the MAC
+ * of block_gfni / block_avx2 over the k survivors.  Layout of
+ * memo_ec_rebuild_batch.  Returns the ISA used, or -1 (bad pattern). */
+typedef struct {
+    int isa, k, m, e;
+    size_t S, b0, b1;
+    const uint8_t *sidx, *surv, *lidx;
+    uint8_t *out;
+    int rc;
+} rebuild_job;
+
+static void *rebuild_thread(void *arg)
+{
+    rebuild_job *r = (rebuild_job *)arg;
+    const int k = r->k, e = r->e;
+    uint8_t *rows = (uint8_t *)malloc((size_t)e * k);
+    uint64_t *aff = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)e * k);
+    uint8_t *nib = (uint8_t *)malloc((size_t)e * k * 32);
+    for (size_t b = r->b0; b < r->b1; ++b) {
+        if (memo_oracle_decode_matrix(k, r->m, r->sidx + b * k, r->lidx + b * e, e, rows)) {
+            r->rc = -1;
+            break;
+        }
+        for (int i = 0; i < e * k; ++i) {
+            if (r->isa == ISA_GFNI512) aff[i] = affine_matrix(rows[i]);
+            else if (r->isa == ISA_AVX2)
+                for (int v = 0; v < 16; ++v) {
+                    nib[(size_t)i * 32 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)v);
+                    nib[(size_t)i * 32 + 16 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)(v << 4));
+                }
+        }
+        const simd_job j = {r->isa, k, e, r->S, 0, 0, NULL, NULL, rows, aff, nib};
+        const uint8_t *d = r->surv + b * (size_t)k * r->S;
+        uint8_t *o = r->out + b * (size_t)e * r->S;
+        if (r->isa == ISA_GFNI512) block_gfni(&j, d, o);
+        else if (r->isa == ISA_AVX2) block_avx2(&j, d, o);
+        else scalar_cols(&j, d, o, 0);
+    }
+    if (r->isa == ISA_GFNI512) sfence_all();
+    free(rows); free(aff); free(nib);
+    return NULL;
+}
+
+int memo_oracle_rebuild_simd_mt(int k, int m, size_t S, size_t n, const uint8_t *surv_idx,
+                                const uint8_t *surv, const uint8_t *lost_idx, int e,
+                                uint8_t *out, int threads, int isa)
+{
+    if (k < 1 || m < 1 || k + m > 256 || e < 1 || e > m) return -1;
+    const int best = memo_oracle_simd_isa();
+    if (isa < 0 || isa > best) isa = best;
+    if (threads < 1) threads = 1;
+    if ((size_t)threads > n && n > 0) threads = (int)n;
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)threads);
+    rebuild_job *jobs = (rebuild_job *)malloc(sizeof(rebuild_job) * (size_t)threads);
+    for (int t = 0; t < threads; ++t) {
+        jobs[t] = (rebuild_job){isa, k, m, e, S, n * (size_t)t / (size_t)threads,
+                                n * (size_t)(t + 1) / (size_t)threads, surv_idx, surv, lost_idx, out, 0};
+        pthread_create(&th[t], NULL, rebuild_thread, &jobs[t]);
+    }
+    int rc = isa;
+    for (int t = 0; t < threads; ++t) {
+        pthread_join(th[t], NULL);
+        if (jobs[t].rc) rc = -1;
+    }
+    free(th); free(jobs);
+    return rc;
 }

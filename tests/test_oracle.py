@@ -210,3 +210,20 @@ def test_c_oracle_matches_headline_digests(O):
                 assert list(s[0]) == r["surv"] and list(l[0]) == r["lost"]
                 out = O.rebuild(k, m, S, s, O.gather(k, m, S, data, par, s), l)
                 assert sha(out) == r["out_sha256"], (bt["name"], b, r["e"])
+
+
+@pytest.mark.parametrize("k,m,B", [(10, 4, 100000), (3, 2, 65536), (16, 4, 4096), (5, 3, 777)])
+def test_simd_rebuild_matches_scalar(O, k, m, B):
+    """oracle/rs_simd.c's rebuild (the CPU baseline of the rebuild configs)
+    is bit-exact with the scalar oracle on every ISA this CPU has."""
+    S = O.shard_size(B, k)
+    n = 9
+    data = O.fill_blocks(SEED, 3, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    for e in sorted({1, m}):
+        s, l = O.erasures(SEED, 3, n, k, m, e)
+        surv = O.gather(k, m, S, data, par, s)
+        want = O.gather(k, m, S, data, par, l)
+        for isa in range(O.simd_isa() + 1):
+            out, used = O.rebuild_simd(k, m, S, s, surv, l, threads=3, isa=isa)
+            assert used == isa and np.array_equal(out, want), (k, m, B, e, isa)
