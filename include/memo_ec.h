@@ -134,7 +134,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
  * blocks, as the encode's parity rows are, so the call runs at encode
  * speed.  An invalid pattern (duplicate or out-of-range index) returns
  * MEMO_EC_ESINGULAR before anything is enqueued.  `where` as for
- * memo_ec_rebuild_batch (surv/out memory only). */
+ * memo_ec_rebuild_batch (surv/out memory only).  The ctx caches the tables
+ * of its last 64 patterns; a pattern's first call uploads them
+ * synchronously, so make that call before capturing a HIP graph. */
 int memo_ec_rebuild_uniform(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
                             const uint8_t *surv_idx, const uint8_t *surv,
                             const uint8_t *lost_idx, int e, uint8_t *out,

@@ -112,6 +112,13 @@ def test_batches_split_across_launches(codec, O, monkeypatch, rebuild_path):
     codec.rebuild(k, m, dev(s), dev(surv), dev(l), out)
     codec.synchronize()
     assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
+    # one pattern for every block (memo_ec_rebuild_uniform), split the same way
+    su, lu = s[0], l[0]
+    svu = O.gather(k, m, S, data, want, np.tile(su, (n, 1)))
+    outu = empty(n, 3 * S)
+    codec.rebuild_uniform(k, m, su, dev(svu), lu, outu)
+    codec.synchronize()
+    assert np.array_equal(host(outu), O.gather(k, m, S, data, want, np.tile(lu, (n, 1))))
 
 
 def test_c1_full_size_vs_oracle(codec, O):
@@ -500,6 +507,16 @@ def test_hip_graph_capture_replay(codec, O):
         codec.gather_shards(k, m, S, n, d, p, sd, surv)
         codec.rebuild(k, m, sd, surv, ld, out)
     torch.cuda.synchronize()
+    # the uniform rebuild's table image is formed on its first call, before
+    # capture (a capture may only enqueue work)
+    su, lu = s[0], l[0]
+    sdu = dev(np.tile(su, (n, 1)))
+    survu = empty(n, k * S)
+    outu = empty(n, e * S)
+    with torch.cuda.stream(st):
+        codec.gather_shards(k, m, S, n, d, p, sdu, survu)
+        codec.rebuild_uniform(k, m, su, survu, lu, outu)
+    torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         cs = torch.cuda.current_stream()
@@ -507,6 +524,8 @@ def test_hip_graph_capture_replay(codec, O):
         codec.encode(k, m, d, p)
         codec.gather_shards(k, m, S, n, d, p, sd, surv)
         codec.rebuild(k, m, sd, surv, ld, out)
+        codec.gather_shards(k, m, S, n, d, p, sdu, survu)
+        codec.rebuild_uniform(k, m, su, survu, lu, outu)
     codec.set_stream(None)
     for fb in [100, 200]:
         codec.fill_blocks(SEED, fb, n, B, k, S, d)
@@ -517,6 +536,7 @@ def test_hip_graph_capture_replay(codec, O):
         want = O.encode(k, m, S, data)
         assert np.array_equal(host(p), want)
         assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
+        assert np.array_equal(host(outu), O.gather(k, m, S, data, want, np.tile(lu, (n, 1))))
 
 
 def test_concurrent_contexts_from_threads(O):
