@@ -40,29 +40,6 @@ struct PhaseTimer {
   }
 };
 
-// Batch scratch whose bytes are all written before they are read: a vector
-// that default-initialises (no zero fill of hundreds of MB on one thread;
-// the padding is zeroed where it is written).
-template <class T>
-struct NoInitAlloc : std::allocator<T> {
-  template <class U>
-  struct rebind {
-    using other = NoInitAlloc<U>;
-  };
-  NoInitAlloc() = default;
-  template <class U>
-  NoInitAlloc(const NoInitAlloc<U>&) {}
-  template <class U>
-  void construct(U* p) noexcept {
-    ::new (static_cast<void*>(p)) U;
-  }
-  template <class U, class... A>
-  void construct(U* p, A&&... a) {
-    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
-  }
-};
-using Scratch = std::vector<uint8_t, NoInitAlloc<uint8_t>>;
-
 // Block payload d as k shards of Sb bytes into k slots of S >= Sb bytes at
 // dst (memo_ec_shard_size padding and the slot tails zeroed).
 void copy_padded(const Buffer& d, int k, size_t Sb, uint8_t* dst, size_t S) {
@@ -168,11 +145,12 @@ void Codec::split(size_t n, const std::function<int(size_t, size_t, size_t)>& fn
   for (int r : rc) check(r, what);
 }
 
-void Codec::encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity) {
+void Codec::encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity,
+                   bool pinned) {
   split(n, [&](size_t d, size_t b0, size_t cnt) {
     auto* c = acquire(d);
     const int rc = memo_ec_encode_batch(c, k, m, S, cnt, data + b0 * k * S, parity + b0 * m * S,
-                                        MEMO_EC_HOST);
+                                        pinned ? MEMO_EC_HOST_PINNED : MEMO_EC_HOST);
     release(d, c);
     return rc;
   }, "encode");
@@ -180,11 +158,12 @@ void Codec::encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_
 }
 
 void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
-                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out) {
+                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out, bool pinned) {
   split(n, [&](size_t d, size_t b0, size_t cnt) {
     auto* c = acquire(d);
     const int rc = memo_ec_rebuild_batch(c, k, m, S, cnt, surv_idx + b0 * k, surv + b0 * k * S,
-                                         lost_idx + b0 * e, e, out + b0 * e * S, MEMO_EC_HOST);
+                                         lost_idx + b0 * e, e, out + b0 * e * S,
+                                         pinned ? MEMO_EC_HOST_PINNED : MEMO_EC_HOST);
     release(d, c);
     return rc;
   }, "rebuild");
@@ -192,15 +171,81 @@ void Codec::rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
 }
 
 void Codec::rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
-                            const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out) {
+                            const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
+                            bool pinned) {
   split(n, [&](size_t d, size_t b0, size_t cnt) {
     auto* c = acquire(d);
     const int rc = memo_ec_rebuild_uniform(c, k, m, S, cnt, surv_idx, surv + b0 * k * S, lost_idx, e,
-                                           out + b0 * e * S, MEMO_EC_HOST);
+                                           out + b0 * e * S,
+                                           pinned ? MEMO_EC_HOST_PINNED : MEMO_EC_HOST);
     release(d, c);
     return rc;
   }, "rebuild_uniform");
   ++uniform_calls_;
+}
+
+// ------------------------------------------------------- pinned arena
+PinnedArena::Lease& PinnedArena::Lease::operator=(Lease&& o) noexcept {
+  if (this != &o) {
+    if (a_ && p_) a_->put(p_, cap_, pinned_);
+    a_ = o.a_;
+    p_ = o.p_;
+    cap_ = o.cap_;
+    pinned_ = o.pinned_;
+    o.a_ = nullptr;
+    o.p_ = nullptr;
+  }
+  return *this;
+}
+
+PinnedArena::Lease::~Lease() {
+  if (a_ && p_) a_->put(p_, cap_, pinned_);
+}
+
+void PinnedArena::release(const Buf& b) {
+  if (b.pinned) memo_ec_host_free(b.p);
+  else std::free(b.p);
+}
+
+PinnedArena::~PinnedArena() {
+  for (auto& b : free_) release(b);
+}
+
+PinnedArena::Lease PinnedArena::lease(size_t bytes) {
+  bytes = std::max<size_t>(bytes, 64);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    size_t best = free_.size();
+    for (size_t i = 0; i < free_.size(); ++i)
+      if (free_[i].cap >= bytes && (best == free_.size() || free_[i].cap < free_[best].cap)) best = i;
+    if (best != free_.size()) {
+      const Buf b = free_[best];
+      free_.erase(free_.begin() + best);
+      return Lease(this, b.p, b.cap, b.pinned);
+    }
+  }
+  // round up (fewer distinct sizes to keep) and pin; ordinary memory if the
+  // pinned allocation fails
+  const size_t cap = bytes <= (1u << 20) ? (size_t)1 << 20 : (bytes + (16u << 20) - 1) & ~(size_t)((16u << 20) - 1);
+  if (void* p = memo_ec_host_alloc(cap)) return Lease(this, static_cast<uint8_t*>(p), cap, true);
+  void* p = std::malloc(cap);
+  if (!p) throw Error("erasure: out of host memory");
+  return Lease(this, static_cast<uint8_t*>(p), cap, false);
+}
+
+void PinnedArena::put(uint8_t* p, size_t cap, bool pinned) {
+  Buf drop{nullptr, 0, false};
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    free_.push_back({p, cap, pinned});
+    if (free_.size() > keep_) {  // keep the largest buffers
+      auto small = std::min_element(free_.begin(), free_.end(),
+                                    [](const Buf& a, const Buf& b) { return a.cap < b.cap; });
+      drop = *small;
+      free_.erase(small);
+    }
+  }
+  if (drop.p) release(drop);
 }
 
 // ---------------------------------------------------------- shard format
@@ -565,17 +610,17 @@ void ErasureConsensus::batcher_loop() {
       size_t S = 0;
       for (auto* j : g.second) S = std::max(S, memo_ec_shard_size(j->block->data.size(), o_.k));
       try {
-        Scratch data(n * o_.k * S), parity(n * o_.m * S);
+        auto data = arena_.lease(n * o_.k * S), parity = arena_.lease(n * o_.m * S);
         for (size_t i = 0; i < n; ++i) {
           const auto& d = g.second[i]->block->data;
           copy_padded(d, o_.k, memo_ec_shard_size(d.size(), o_.k), data.data() + i * o_.k * S, S);
         }
-        codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
+        codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data(), data.pinned() && parity.pinned());
         for (size_t i = 0; i < n; ++i) {
           const size_t Sb = memo_ec_shard_size(g.second[i]->block->data.size(), o_.k);
           Buffer p((size_t)o_.m * Sb);
           for (int r = 0; r < o_.m; ++r)
-            std::copy(parity.begin() + (i * o_.m + r) * S, parity.begin() + (i * o_.m + r) * S + Sb,
+            std::copy(parity.data() + (i * o_.m + r) * S, parity.data() + (i * o_.m + r) * S + Sb,
                       p.begin() + (size_t)r * Sb);
           g.second[i]->parity.set_value(std::move(p));
         }
@@ -680,14 +725,14 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
       const size_t n = g.second.size();
       size_t S = 0;
       for (auto* b : g.second) S = std::max(S, memo_ec_shard_size(b->data.size(), o_.k));
-      Scratch data(n * o_.k * S), parity(n * o_.m * S);
+      auto data = arena_.lease(n * o_.k * S), parity = arena_.lease(n * o_.m * S);
       tm.lap("alloc");
       pool_.parallel_for(n, [&](size_t i) {
         const auto& d = g.second[i]->data;
         copy_padded(d, o_.k, memo_ec_shard_size(d.size(), o_.k), data.data() + i * o_.k * S, S);
       });
       tm.lap("copy_in");
-      codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data());
+      codec_.encode(o_.k, o_.m, S, n, data.data(), parity.data(), data.pinned() && parity.pinned());
       tm.lap("encode");
       // shards straight from the batch buffers (a block's shard is the first
       // Sb bytes of its S-byte slot)
@@ -954,7 +999,8 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
       for (size_t bi = 0; bi < nb; ++bi) S = std::max(S, (size_t)g[ids[b0 + bi]].h.shard_size);
       std::vector<uint8_t> sidx(nb * k), lidx(nb * e);
-      Scratch surv(nb * k * S), out(nb * e * S);
+      auto surv = arena_.lease(nb * k * S), out = arena_.lease(nb * e * S);
+      const bool pin = surv.pinned() && out.pinned();
       tm.lap("alloc");
       pool_.parallel_for(nb, [&](size_t bi) {
         Gathered& x = g[ids[b0 + bi]];
@@ -969,9 +1015,9 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       tm.lap("copy_in");
       if (grp.uniform)
         codec_.rebuild_uniform(k, m, S, nb, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
-                               out.data());
+                               out.data(), pin);
       else
-        codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data());
+        codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data(), pin);
       tm.lap("rebuild");
       decoded_ += nb;
       pool_.parallel_for(nb, [&](size_t bi) { finish(ids[b0 + bi], out.data() + bi * e * S, S); });
@@ -1125,7 +1171,8 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
         for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(grp.items[b0 + bi]->pl.B, k));
         std::vector<uint8_t> sidx(n * k), lidx(n * e);
-        Scratch surv(n * k * S), out(n * e * S);
+        auto surv = arena_.lease(n * k * S), out = arena_.lease(n * e * S);
+        const bool pin = surv.pinned() && out.pinned();
         pool_.parallel_for(n, [&](size_t bi) {
           Todo& x = *grp.items[b0 + bi];
           const size_t Sb = memo_ec_shard_size(x.pl.B, k);
@@ -1141,9 +1188,9 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         });
         if (grp.uniform)
           codec_.rebuild_uniform(k, m, S, n, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
-                                 out.data());
+                                 out.data(), pin);
         else
-          codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data());
+          codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data(), pin);
         ++rep.codec_calls;
         std::vector<int> placed(n, 0);
         // place each rebuilt shard on a reachable node holding none of the

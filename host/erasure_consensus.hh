@@ -47,13 +47,17 @@ class Codec {
   ~Codec();
   Codec(const Codec&) = delete;
   Codec& operator=(const Codec&) = delete;
-  void encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity);
+  // pinned: both buffers come from memo_ec_host_alloc (MEMO_EC_HOST_PINNED:
+  // the library DMAs straight from them, no bounce copies)
+  void encode(int k, int m, size_t S, size_t n, const uint8_t* data, uint8_t* parity,
+              bool pinned = false);
   void rebuild(int k, int m, size_t S, size_t n, const uint8_t* surv_idx, const uint8_t* surv,
-               const uint8_t* lost_idx, int e, uint8_t* out);
+               const uint8_t* lost_idx, int e, uint8_t* out, bool pinned = false);
   // One erasure pattern for all n blocks (memo_ec_rebuild_uniform):
   // surv_idx has k entries, lost_idx e.
   void rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
-                       const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out);
+                       const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
+                       bool pinned = false);
   uint64_t encode_calls() const { return encode_calls_; }
   uint64_t rebuild_calls() const { return rebuild_calls_; }
   uint64_t uniform_calls() const { return uniform_calls_; }
@@ -75,6 +79,50 @@ class Codec {
   std::vector<Dev> dev_;
   std::atomic<size_t> rr_{0};
   std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0}, uniform_calls_{0};
+};
+
+// ------------------------------------------------------- pinned arena
+// Reusable page-locked batch buffers (memo_ec_host_alloc).  The codec's
+// host-memory calls then DMA straight from them (no staging copies in the
+// library), and no batch pays for fresh pages or their release.  A buffer
+// that cannot be pinned falls back to ordinary memory (pinned() false).
+class PinnedArena {
+ public:
+  class Lease {
+   public:
+    Lease() = default;
+    Lease(PinnedArena* a, uint8_t* p, size_t cap, bool pinned) : a_(a), p_(p), cap_(cap), pinned_(pinned) {}
+    Lease(Lease&& o) noexcept { *this = std::move(o); }
+    Lease& operator=(Lease&& o) noexcept;
+    Lease(const Lease&) = delete;
+    Lease& operator=(const Lease&) = delete;
+    ~Lease();
+    uint8_t* data() const { return p_; }
+    bool pinned() const { return pinned_; }
+
+   private:
+    PinnedArena* a_ = nullptr;
+    uint8_t* p_ = nullptr;
+    size_t cap_ = 0;
+    bool pinned_ = false;
+  };
+  explicit PinnedArena(size_t keep = 8) : keep_(keep) {}
+  ~PinnedArena();
+  PinnedArena(const PinnedArena&) = delete;
+  PinnedArena& operator=(const PinnedArena&) = delete;
+  Lease lease(size_t bytes);
+
+ private:
+  struct Buf {
+    uint8_t* p;
+    size_t cap;
+    bool pinned;
+  };
+  void put(uint8_t* p, size_t cap, bool pinned);
+  static void release(const Buf& b);
+  std::mutex mu_;
+  std::vector<Buf> free_;
+  size_t keep_;
 };
 
 // ---------------------------------------------------------- shard format
@@ -275,6 +323,7 @@ class ErasureConsensus : public StackedConsensus {
   Overlay& overlay_;
   ErasureOptions o_;
   Codec codec_;
+  PinnedArena arena_;  // batch buffers of the codec calls
   ThreadPool pool_;
   mutable std::shared_mutex index_mu_;  // readers: fetch paths; writers: place, repair, remove
   std::unordered_map<Address, Placement, AddressHash> index_;  // Paxos::_quorums analogue

@@ -124,6 +124,12 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
                           const uint8_t *lost_idx, int e, uint8_t *out,
                           int where);
 
+/* Page-locked host memory for MEMO_EC_HOST_PINNED calls (hipHostMalloc):
+ * batch buffers the caller reuses, so its host-memory calls skip the
+ * library's bounce copies.  NULL on failure.  Free with memo_ec_host_free. */
+void *memo_ec_host_alloc(size_t bytes);
+int memo_ec_host_free(void *p);
+
 /* Rebuild with ONE erasure pattern for the whole batch: every block lost the
  * shards lost_idx[0..e) and is rebuilt from the survivors surv_idx[0..k)
  * (host pointers: k and e bytes), surv n x k x S in surv_idx order, out

@@ -866,6 +866,17 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
                   });
 }
 
+void* memo_ec_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (bytes == 0 || hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) return nullptr;
+  return p;
+}
+
+int memo_ec_host_free(void* p) {
+  if (!p) return MEMO_EC_OK;
+  return hip_rc(hipHostFree(p));
+}
+
 int memo_ec_rebuild_uniform(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
                             const uint8_t* surv_idx, const uint8_t* surv, const uint8_t* lost_idx,
                             int e, uint8_t* out, int where) {

@@ -48,7 +48,8 @@ _LIB = None
 EXPORTS = [
     "memo_ec_ctx_create", "memo_ec_ctx_destroy", "memo_ec_set_stream", "memo_ec_get_stream",
     "memo_ec_synchronize", "memo_ec_shard_size", "memo_ec_generator", "memo_ec_encode_batch",
-    "memo_ec_rebuild_batch", "memo_ec_rebuild_uniform", "memo_ec_decode_rows", "memo_ec_encode_segments",
+    "memo_ec_rebuild_batch", "memo_ec_rebuild_uniform", "memo_ec_decode_rows",
+    "memo_ec_host_alloc", "memo_ec_host_free", "memo_ec_encode_segments",
     "memo_ec_sha256_batch", "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards",
     "memo_ec_strerror",
     "memo_ec_version", "memo_ec_device_count",
@@ -76,6 +77,9 @@ def _lib():
                                             _u8p, c_int, _u8p, c_int]
         L.memo_ec_rebuild_uniform.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p,
                                               _u8p, c_int, _u8p, c_int]
+        L.memo_ec_host_alloc.argtypes = [_sz]
+        L.memo_ec_host_alloc.restype = ctypes.c_void_p
+        L.memo_ec_host_free.argtypes = [ctypes.c_void_p]
         L.memo_ec_decode_rows.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _u8p, _u8p, c_int, _u8p]
         L.memo_ec_encode_segments.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(Segment)]
         L.memo_ec_sha256_batch.argtypes = [ctypes.c_void_p, _sz, _u8p, _sz, _sz, _u8p, _sz,
