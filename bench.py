@@ -559,7 +559,7 @@ def main():
     if e > 0:
         row["rebuild"] = kstats(kms[1], (k + e) * S * n)
         row["rebuild_bit_exact"] = bool(torch.equal(out, want))
-        row["rebuild_kernel"] = ec.rebuild_kernel_name()
+        row["rebuild_kernel"] = ec.rebuild_kernel_name(n, k, S)
         del surv, out, want
     rows = [row]
     wall_max = wall

@@ -263,16 +263,21 @@ int lw0_table(memo_ec_ctx* ctx, int k, int m, const uint32_t** out) {
   return MEMO_EC_OK;
 }
 
-// 0 (default): the two-kernel rebuild, decode_coef_kernel rows through HBM
-// + gf_mac_kernel; 1: one fused launch (gf_rebuild_kernel) whose tiles
-// derive their blocks' rows themselves (MEMO_EC_REBUILD_FUSED, read per
-// call).  Measured (profiles/r02_rebuild_pmc.md): the MAC is ~75% VALU-busy,
-// and the fused decode's VALU/LDS work costs more than the decode kernel
-// and the rows' HBM round trip it removes -- C3 1054 vs 1012 us, 4 KiB
-// RS(10,4) 1239 vs 1186 us, 4 KiB RS(16,4) 1059 vs 1063 us.
-bool rebuild_fused() {
-  const char* p = std::getenv("MEMO_EC_REBUILD_FUSED");
-  return p && std::atoi(p) != 0;
+// The device rebuild path of a call moving `in_bytes` of survivors:
+//  - fused (gf_rebuild_kernel: each tile derives its blocks' decode rows, one
+//    launch) for calls up to MEMO_EC_FUSED_MAX_MB (64) MiB: latency-bound,
+//    the saved launch wins (one-block degraded reads: 4 KiB 27-30 -> 23 us,
+//    1 MiB 78-88 -> 62-72 us, profiles/r02_host_latency_fused_ab.jsonl);
+//  - two kernels (decode_coef*/decode_rows_k rows through HBM, then
+//    gf_mac_kernel) above: the MAC is ~75% VALU-busy and the fused decode's
+//    VALU/LDS work costs more than the decode kernel it removes (C3 1054 vs
+//    1012 us, 4 KiB RS(10,4) 1239 vs 1186 us, profiles/r02_rebuild_pmc.md).
+// MEMO_EC_REBUILD_FUSED=0/1 forces one path (read per call: A/B and tests).
+bool rebuild_fused(size_t in_bytes) {
+  if (const char* p = std::getenv("MEMO_EC_REBUILD_FUSED")) return std::atoi(p) != 0;
+  size_t max_mb = 64;
+  if (const char* p = std::getenv("MEMO_EC_FUSED_MAX_MB")) max_mb = std::strtoull(p, nullptr, 10);
+  return in_bytes <= (max_mb << 20);
 }
 
 int sync_pipeline(memo_ec_ctx* ctx);
@@ -929,7 +934,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
-  const bool fused = rebuild_fused();
+  const bool fused = rebuild_fused(n * (size_t)k * S);
   if (where == MEMO_EC_DEVICE) {
     if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
     if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, fused, c->d_tabs,

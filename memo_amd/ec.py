@@ -122,13 +122,19 @@ def erasures(seed, first_block, n, k, m, e):
     return s, l[:, :e].copy()
 
 
-def rebuild_path():
+def rebuild_path(n=None, k=None, S=None):
     """Which device rebuild the library runs (memo_ec.cpp rebuild_fused):
-    'rows' (default) -- decode_coef_kernel rows through HBM, then
-    gf_mac_kernel; 'fused' -- one gf_rebuild_kernel launch whose tiles derive
-    their blocks' decode rows from the indices (MEMO_EC_REBUILD_FUSED=1)."""
+    'fused' -- one gf_rebuild_kernel launch whose tiles derive their blocks'
+    decode rows (calls of up to MEMO_EC_FUSED_MAX_MB = 64 MiB of survivors);
+    'rows' -- decode rows through HBM, then gf_mac_kernel (larger calls).
+    MEMO_EC_REBUILD_FUSED=0/1 forces one."""
     v = os.environ.get("MEMO_EC_REBUILD_FUSED")
-    return "fused" if v is not None and _atoi(v) != 0 else "rows"
+    if v is not None:
+        return "fused" if _atoi(v) != 0 else "rows"
+    if None in (n, k, S):
+        return "auto"
+    max_mb = _atoi(os.environ.get("MEMO_EC_FUSED_MAX_MB", "64"))
+    return "fused" if n * k * S <= (max_mb << 20) else "rows"
 
 
 def _atoi(v):
@@ -138,9 +144,11 @@ def _atoi(v):
         return 0
 
 
-def rebuild_kernel_name():
+def rebuild_kernel_name(n=None, k=None, S=None):
     return {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
-            "rows": "decode_coef_kernel + gf_mac_kernel (rows through HBM)"}[rebuild_path()]
+            "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM)",
+            "auto": "fused up to 64 MiB per call, else decode rows + gf_mac_kernel"}[
+        rebuild_path(n, k, S)]
 
 
 def _is_torch(x):
