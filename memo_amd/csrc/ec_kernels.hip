@@ -1198,8 +1198,9 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
 // so a block's survivor set is one 32-bit mask; its m non-survivors are
 // extracted once into registers (ctz), every loop is unrolled at compile
 // time (rows r < e by uniform predicates), the rows are packed into dwords
-// before they are staged in LDS, and LW0 comes from the host's per-code
-// table.  The coefficient of (lost l, survivor s) costs one XOR, two LDS
+// and stored from registers (rows of whole dwords: each row as soon as it is
+// done; others through LDS when e*K is not a dword multiple), and LW0 comes
+// from the host's per-code table.  The coefficient of (lost l, survivor s) costs one XOR, two LDS
 // lookups and one v_add3_u32:
 //   row_l[t] = EX[lw_t + llam_l + NLG[l ^ s_t]]
 // with NLG = 255 - log (so no subtraction), and log sums kept unreduced
@@ -1213,13 +1214,18 @@ struct DecTables {
   uint8_t lg[256];    // log
   uint8_t nlg[256];   // 255 - log (nlg[0]: 0, never used for a non-unit row)
   uint8_t ex[1280];   // 2^(i mod 255)
+  uint8_t none[256];  // zeros: lg[x ^ kDecNone] for an absent non-survivor
 };
+// index offset that turns lg[x ^ c] into 0 (x < 256): fills the unused
+// slots of the non-survivor list so lookups run in unpredicated groups
+constexpr uint32_t kDecNone = 1792;
 constexpr DecTables make_dec_tables() {
   DecTables t{};
   const GfTables g = make_gf();
   for (int i = 0; i < 256; ++i) {
     t.lg[i] = g.log[i];
     t.nlg[i] = i ? (uint8_t)(255 - g.log[i]) : 0;
+    t.none[i] = 0;
   }
   for (int i = 0; i < 1280; ++i) t.ex[i] = g.exp[i % 255];
   return t;
@@ -1287,7 +1293,11 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
   }
   __syncthreads();
   const uint32_t ek = e * K;
-  uint32_t* out = reinterpret_cast<uint32_t*>(s_out + tid * a.pitch);
+  // the rows go to global memory straight from registers when they are
+  // whole dwords (pitch 0, set by the launcher), else through LDS
+  const bool direct = a.pitch == 0;
+  constexpr int kW = (MEMO_EC_MAX_M * K + 3) / 4;
+  uint32_t wd[kW];
   if (live) {
     // survivor set: a duplicate leaves fewer than K bits, an index >= nt a
     // bit at or past nt (or past 31: caught by the OR of all indices)
@@ -1309,29 +1319,35 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
     uint32_t cl[MEMO_EC_MAX_M];
 #pragma unroll
     for (int q = 0; q < MEMO_EC_MAX_M; ++q) {
-      cl[q] = 0;
+      cl[q] = kDecNone;
       if ((uint32_t)q < m) {
         cl[q] = __builtin_ctz(comp | 0x80000000u);  // a faulty set may run out: 31
         comp &= comp - 1;
       }
     }
-    // log W_t = LW0(s_t) + sum_c log(s_t ^ c), folded once (<= 271)
+    // log W_t = LW0(s_t) + sum_c log(s_t ^ c), folded once (<= 271); the
+    // lookups go in groups of 4 (or 2) independent reads per branch
     uint32_t lw[K];
 #pragma unroll
     for (int t = 0; t < K; ++t) lw[t] = lw0[sv[t] & 31];
 #pragma unroll
-    for (int q = 0; q < MEMO_EC_MAX_M; q += 2) {
-      if ((uint32_t)q + 1 < m) {
+    for (int q = 0; q < MEMO_EC_MAX_M; q += 4) {
+      if ((uint32_t)q + 2 < m) {
 #pragma unroll
-        for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]] + lg[sv[t] ^ cl[q + 1]];
+        for (int t = 0; t < K; ++t)
+          lw[t] += (lg[sv[t] ^ cl[q]] + lg[sv[t] ^ cl[q + 1]]) + (lg[sv[t] ^ cl[q + 2]] + lg[sv[t] ^ cl[q + 3]]);
       } else if ((uint32_t)q < m) {
 #pragma unroll
-        for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]];
+        for (int t = 0; t < K; ++t) lw[t] += lg[sv[t] ^ cl[q]] + lg[sv[t] ^ cl[q + 1]];
       }
     }
 #pragma unroll
     for (int t = 0; t < K; ++t) lw[t] = fold255(lw[t]);
-    // rows, packed 4 bytes per dword
+    // rows, packed 4 bytes per register (compile-time positions); a faulty
+    // block's rows are zero
+    const uint32_t keep = bad ? 0u : ~0u;
+    const bool vec16 = (ek & 15) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 15) == 0;
+    const bool vec8 = (ek & 7) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 7) == 0;
     uint32_t word = 0;
 #pragma unroll
     for (int r = 0; r < MEMO_EC_MAX_M; ++r) {
@@ -1340,9 +1356,11 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
         const bool unit = (mask >> (l & 31)) & 1u;
         uint32_t acc = lw0[l & 31];
 #pragma unroll
-        for (int q = 0; q < MEMO_EC_MAX_M; ++q)
-          if ((uint32_t)q < m) acc += lg[l ^ cl[q]];  // c == l adds log[0] = 0
-        const uint32_t llam = 510u - fold255(acc);   // == -log(Lam_l) mod 255, in [239, 510]
+        for (int q = 0; q < MEMO_EC_MAX_M; q += 4)  // c == l adds log[0] = 0
+          if ((uint32_t)q < m)
+            acc += (lg[l ^ cl[q]] + lg[l ^ cl[q + 1]]) + (lg[l ^ cl[q + 2]] + lg[l ^ cl[q + 3]]);
+        uint32_t llam = 510u - fold255(acc);  // == -log(Lam_l) mod 255, in [239, 510]
+        asm volatile("" : "+v"(llam));  // keep one v_add3_u32 per coefficient
         uint32_t v[K];
         if (!unit) {
 #pragma unroll
@@ -1351,23 +1369,77 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
 #pragma unroll
           for (int t = 0; t < K; ++t) v[t] = sv[t] == l ? 1u : 0u;
         }
+        if constexpr (K % 4 == 0) {
+          // whole dwords per row (3 byte permutes per 4 bytes), stored as
+          // soon as the row is done: no row buffer in registers
+          uint32_t rw[K / 4 + (K < 4)];
+#pragma unroll
+          for (int t = 0; t < K; t += 4) {
+            const uint32_t lo = __builtin_amdgcn_perm(v[t + 1], v[t], 0x0c0c0400u);
+            const uint32_t hi = __builtin_amdgcn_perm(v[t + 3], v[t + 2], 0x0c0c0400u);
+            rw[t / 4] = __builtin_amdgcn_perm(hi, lo, 0x05040100u) & keep;
+          }
+          if (direct) {
+            uint8_t* dst = a.rows + b * ek + (uint32_t)(r * K);
+            if (K % 16 == 0 && vec16) {
+#pragma unroll
+              for (int w = 0; w < K / 4; w += 4)
+                reinterpret_cast<uint4*>(dst)[w / 4] = make_uint4(rw[w], rw[w + 1], rw[w + 2], rw[w + 3]);
+            } else if (K % 8 == 0 && vec8) {
+#pragma unroll
+              for (int w = 0; w < K / 4; w += 2) reinterpret_cast<uint2*>(dst)[w / 2] = make_uint2(rw[w], rw[w + 1]);
+            } else {
+#pragma unroll
+              for (int w = 0; w < K / 4; ++w) reinterpret_cast<uint32_t*>(dst)[w] = rw[w];
+            }
+          } else {
+            uint32_t* out = reinterpret_cast<uint32_t*>(s_out + tid * a.pitch) + r * (K / 4);
+#pragma unroll
+            for (int w = 0; w < K / 4; ++w) out[w] = rw[w];
+          }
+          continue;
+        }
 #pragma unroll
         for (int t = 0; t < K; ++t) {
           const int q = r * K + t;  // compile-time byte position
           word |= v[t] << (8 * (q & 3));
           if ((q & 3) == 3) {
-            out[q >> 2] = word;
+            wd[q >> 2] = word & keep;
             word = 0;
+          } else if (t == K - 1 && (uint32_t)r + 1 == e) {
+            wd[q >> 2] = word & keep;  // the partial last dword
           }
         }
       }
     }
-    if ((ek & 3) != 0) out[ek >> 2] = word;  // the partial last dword
-    if (bad) {
-      for (uint32_t w = 0; w < (ek + 3) / 4; ++w) out[w] = 0;
-      if (a.status) *a.status = 1u;  // plain store: every writer stores 1
+    if (bad && a.status) *a.status = 1u;  // plain store: every writer stores 1
+    if (K % 4 == 0) {
+      // rows already stored
+    } else if (direct) {
+      // ek % 4 == 0 and a 4-aligned base (launcher); widest stores that fit
+      uint8_t* dst = a.rows + b * ek;
+      if (vec16) {
+#pragma unroll
+        for (int w = 0; w + 3 < kW; w += 4)
+          if ((uint32_t)w * 4 < ek)
+            reinterpret_cast<uint4*>(dst)[w >> 2] = make_uint4(wd[w], wd[w + 1], wd[w + 2], wd[w + 3]);
+      } else if (vec8) {
+#pragma unroll
+        for (int w = 0; w + 1 < kW; w += 2)
+          if ((uint32_t)w * 4 < ek) reinterpret_cast<uint2*>(dst)[w >> 1] = make_uint2(wd[w], wd[w + 1]);
+      } else {
+#pragma unroll
+        for (int w = 0; w < kW; ++w)
+          if ((uint32_t)w * 4 < ek) reinterpret_cast<uint32_t*>(dst)[w] = wd[w];
+      }
+    } else {
+      uint32_t* out = reinterpret_cast<uint32_t*>(s_out + tid * a.pitch);
+#pragma unroll
+      for (int w = 0; w < kW; ++w)
+        if ((uint32_t)w * 4 < ek) out[w] = wd[w];
     }
   }
+  if (direct) return;
   __syncthreads();
   // this workgroup's rows are one contiguous range of nb * ek bytes
   const uint64_t nb = a.n - b0 < 256 ? a.n - b0 : 256;
@@ -1377,8 +1449,7 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
     const uint32_t ekw = ek >> 2;
     for (uint32_t w = tid; w < (total >> 2); w += 256) {
       const uint32_t lb = w / ekw, off = w - lb * ekw;
-      reinterpret_cast<uint32_t*>(dst)[w] =
-          *reinterpret_cast<const uint32_t*>(s_out + lb * a.pitch + off * 4);
+      reinterpret_cast<uint32_t*>(dst)[w] = *reinterpret_cast<const uint32_t*>(s_out + lb * a.pitch + off * 4);
     }
   } else {
     for (uint32_t x = tid; x < total; x += 256) {
@@ -1785,11 +1856,18 @@ hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   // per call, for A/B runs and tests)
   const char* ex_env = std::getenv("MEMO_EC_DECODE_EXACT");
   const bool exact = !ex_env || std::atoi(ex_env) != 0;
-  if (exact && a.pitch && a.lw0 && a.k + a.m <= 32) {
+  // exact-k kernels store whole-dword rows straight from registers
+  // (MEMO_EC_DECODE_STAGE=1: through LDS, for A/B runs)
+  const char* st_env = std::getenv("MEMO_EC_DECODE_STAGE");
+  const bool stage = st_env && std::atoi(st_env) != 0;
+  DecodeArgs ax = a;
+  if (!stage && (ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) ax.pitch = 0;
+  if (exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32) {
+    const size_t xlds = ax.pitch ? lds : 0;
     switch (a.k) {
 #define MEMO_EC_DK(x)                                                                    \
   case x:                                                                                \
-    hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), lds, st, a);      \
+    hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), xlds, st, ax);    \
     return hipGetLastError();
       MEMO_EC_DK(2) MEMO_EC_DK(3) MEMO_EC_DK(4) MEMO_EC_DK(6) MEMO_EC_DK(8) MEMO_EC_DK(10)
       MEMO_EC_DK(12) MEMO_EC_DK(14) MEMO_EC_DK(16)

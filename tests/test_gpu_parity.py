@@ -165,7 +165,7 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
 
 @pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 2), (4, 2), (6, 3), (7, 5), (8, 8), (10, 4),
                                  (12, 4), (14, 2), (16, 4), (16, 16), (20, 8), (33, 12), (64, 16)])
-@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_generic"])
+@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_staged", "per_block_generic"])
 def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
     """Closed-form decode rows against the oracle's Gauss-Jordan rows
     C[lost] * inv(C[surv]): random survivor orders, lost shards that are
@@ -174,11 +174,15 @@ def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
     (decode_coef_wide_kernel, small batches) and one lane per block
     (forced by MEMO_EC_DECODE_WIDE_MAX=0: decode_rows_k_kernel for k in
     {2, 3, 4, 6, 8, 10, 12, 14, 16}, decode_coef_kernel otherwise or with
-    MEMO_EC_DECODE_EXACT=0)."""
+    MEMO_EC_DECODE_EXACT=0).  The exact-k kernel stores whole-dword rows
+    from registers, other rows through LDS (all of them with
+    MEMO_EC_DECODE_STAGE=1)."""
     if kernel != "wide":
         monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
     if kernel == "per_block_generic":
         monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
+    if kernel == "per_block_staged":
+        monkeypatch.setenv("MEMO_EC_DECODE_STAGE", "1")
     rng = np.random.default_rng(k * 1000 + m)
     n = 700
     for e in sorted({1, (m + 1) // 2, m}):
@@ -331,7 +335,7 @@ def test_singular_survivors_reported(codec, rebuild_path):
     codec.synchronize()  # error is cleared
 
 
-@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_generic"])
+@pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_staged", "per_block_generic"])
 def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
     """Duplicate survivors, a survivor index >= k+m and a lost index >= k+m
     zero that block's rows (only that block's) and raise ESINGULAR once."""
@@ -340,6 +344,8 @@ def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
         monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
     if kernel == "per_block_generic":
         monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
+    if kernel == "per_block_staged":
+        monkeypatch.setenv("MEMO_EC_DECODE_STAGE", "1")
     k, m, e = 10, 4, 2
     surv = np.array([list(range(10)), [0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [0, 1, 2, 3, 4, 5, 6, 7, 8, 14],
                      [13, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(10))], np.uint8)
