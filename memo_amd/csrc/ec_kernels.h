@@ -48,6 +48,12 @@
 #define MEMO_EC_MAC_COEF_SOA 1
 #endif
 
+// 1: rebuild table images read from a 5 KiB table of all 256 images in
+// global memory (L1/L2-resident) instead of computed per coefficient
+#ifndef MEMO_EC_MAC_IMGTAB
+#define MEMO_EC_MAC_IMGTAB 0
+#endif
+
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
 #endif
@@ -60,6 +66,7 @@ constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
 constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
 constexpr bool MAC_COEF4 = MEMO_EC_MAC_COEF4 != 0;
 constexpr bool MAC_COEF_SOA = MEMO_EC_MAC_COEF_SOA != 0;
+constexpr bool MAC_IMGTAB = MEMO_EC_MAC_IMGTAB != 0;
 // Table dwords per lane staged through registers ahead of the shard loads.
 constexpr int MAC_TAB_REGS = 2;
 // Coefficients per lane staged through registers (rebuild tables built in

@@ -405,6 +405,32 @@ __device__ __forceinline__ void coef_image4(uint32_t c4, uint4 (&q)[4], uint32_t
     q[a] = make_uint4(mid[a], mid[a] ^ bcast_byte(d4, a), hi[a], hi[a] ^ bcast_byte(d7, a));
 }
 
+// The images of all 256 coefficients (q and lo of coef_image), 5 KiB: the
+// rebuild MAC reads a coefficient's image with two loads that hit L1/L2
+// instead of computing it (MAC_IMGTAB).
+struct ImgTable {
+  uint4 q[256];
+  uint32_t lo[256];
+};
+constexpr uint32_t img_xtime(uint32_t x) { return ((x << 1) ^ ((x >> 7) * 0x11Du)) & 0xFFu; }
+constexpr uint32_t img_pack(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return a | (b << 8) | (c << 16) | (d << 24);
+}
+constexpr ImgTable make_img_table() {
+  ImgTable t{};
+  for (uint32_t c = 0; c < 256; ++c) {
+    uint32_t d[8] = {c, 0, 0, 0, 0, 0, 0, 0};
+    for (int i = 1; i < 8; ++i) d[i] = img_xtime(d[i - 1]);
+    t.q[c].x = img_pack(0, d[2], d[3], d[2] ^ d[3]);
+    t.q[c].y = img_pack(d[4], d[4] ^ d[2], d[4] ^ d[3], d[4] ^ d[3] ^ d[2]);
+    t.q[c].z = img_pack(0, d[5], d[6], d[5] ^ d[6]);
+    t.q[c].w = img_pack(d[7], d[7] ^ d[5], d[7] ^ d[6], d[7] ^ d[6] ^ d[5]);
+    t.lo[c] = img_pack(0, d[0], d[1], d[0] ^ d[1]);
+  }
+  return t;
+}
+__constant__ ImgTable kImg = make_img_table();
+
 // Store the image of slot ci (per = R * kpad slots per set).
 __device__ __forceinline__ void put_image(uint32_t* s_tab, const MacSeg& sg, uint32_t per,
                                           uint32_t ci, const uint4& q, uint32_t lo) {
@@ -457,7 +483,20 @@ __device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
                                              const uint32_t (&cv)[MAC_COEF_REGS], uint32_t* s_tab) {
   const uint32_t total = coef_sets(sg, u) * (R * KP);
   const uint32_t t = threadIdx.x;
-  if constexpr (MAC_COEF4) {
+  if constexpr (MAC_IMGTAB) {
+    if (t < total) {  // waves past the tile's slots skip the build
+      uint4 q[MAC_COEF_REGS];
+      uint32_t lo[MAC_COEF_REGS];
+#pragma unroll
+      for (int a = 0; a < MAC_COEF_REGS; ++a) {
+        q[a] = kImg.q[cv[a] & 0xFFu];
+        lo[a] = kImg.lo[cv[a] & 0xFFu];
+      }
+#pragma unroll
+      for (int a = 0; a < MAC_COEF_REGS; ++a)
+        if (t + 256u * a < total) put_image(s_tab, sg, R * KP, t + 256u * a, q[a], lo[a]);
+    }
+  } else if constexpr (MAC_COEF4) {
     static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
     if (t < total) {  // waves past the tile's slots skip the build
       uint4 q[4];
