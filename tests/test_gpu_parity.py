@@ -90,6 +90,51 @@ def test_encode_rebuild_vs_oracle(codec, O, k, m, rebuild_path):
             assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_random_geometries_vs_oracle(codec, O, seed, rebuild_path):
+    """Seeded random codes and sizes (k 1..24, m 1..10, B 1..200000 B, 1..12
+    blocks, any e <= m, every block its own erasure pattern in a random
+    survivor order), device and pageable-host buffers, encode, per-block
+    rebuild and the one-pattern rebuild, all against the oracle."""
+    rng = np.random.default_rng(0xC0DE + seed)
+    for it in range(4):
+        k, m = int(rng.integers(1, 25)), int(rng.integers(1, 11))
+        B = int(rng.integers(1, 200001)) if it else int(rng.integers(1, 64))
+        n = int(rng.integers(1, 13))
+        S = O.shard_size(B, k)
+        fb = int(rng.integers(0, 1 << 20))
+        data = O.fill_blocks(SEED, fb, n, B, k, S)
+        want = O.encode(k, m, S, data)
+        case = (seed, it, k, m, B, n)
+        p = empty(n, m * S)
+        codec.encode(k, m, dev(data), p)
+        ph = np.zeros((n, m * S), np.uint8)
+        codec.encode(k, m, data, ph)
+        codec.synchronize()
+        assert np.array_equal(host(p), want), case
+        assert np.array_equal(ph, want), case
+        e = int(rng.integers(1, m + 1))
+        surv_idx = np.stack([rng.permutation(k + m)[:k] for _ in range(n)]).astype(np.uint8)
+        lost_idx = np.stack([np.setdiff1d(np.arange(k + m), s)[rng.permutation(m)[:e]]
+                             for s in surv_idx]).astype(np.uint8)
+        surv = O.gather(k, m, S, data, want, surv_idx)
+        lost = O.gather(k, m, S, data, want, lost_idx)
+        out = empty(n, e * S)
+        codec.rebuild(k, m, dev(surv_idx), dev(surv), dev(lost_idx), out)
+        oh = np.zeros((n, e * S), np.uint8)
+        codec.rebuild(k, m, surv_idx, surv, lost_idx, oh)
+        codec.synchronize()
+        assert np.array_equal(host(out), lost), case + (e,)
+        assert np.array_equal(oh, lost), case + (e,)
+        # one pattern for the batch: block 0's
+        su = np.repeat(surv_idx[:1], n, axis=0)
+        lu = np.repeat(lost_idx[:1], n, axis=0)
+        ou = empty(n, e * S)
+        codec.rebuild_uniform(k, m, surv_idx[0], dev(O.gather(k, m, S, data, want, su)), lost_idx[0], ou)
+        codec.synchronize()
+        assert np.array_equal(host(ou), O.gather(k, m, S, data, want, lu)), case + (e, "uniform")
+
+
 def test_batches_split_across_launches(codec, O, monkeypatch, rebuild_path):
     """A batch larger than one launch's grid is split into several MAC
     launches (memo_ec.cpp max_blocks_per_launch); the bound is lowered so the
