@@ -342,12 +342,18 @@ ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
   return h;
 }
 
-Key shard_key(const Address& a, int index) {
-  uint8_t tag[16] = {'m', 'e', 'm', 'o', '-', 'e', 'c', '-', 's', 'h', 'a', 'r', 'd', 0, 0, 0};
-  tag[15] = (uint8_t)index;
-  const auto h = sha256(a.value.data(), 32, tag, sizeof tag);
-  return Address(h.data(), flags::immutable_block, true);
+ShardKeys::ShardKeys(const Address& a) {
+  static const uint8_t tag[16] = {'m', 'e', 'm', 'o', '-', 'e', 'c', '-', 's', 'h', 'a', 'r', 'd', 0, 0, 0};
+  base = sha256(a.value.data(), 32, tag, sizeof tag);
 }
+
+Key ShardKeys::operator()(int index) const {
+  std::array<uint8_t, 32> v = base;
+  v[0] ^= (uint8_t)index;
+  return Address(v.data(), flags::immutable_block, true);
+}
+
+Key shard_key(const Address& a, int index) { return ShardKeys(a)(index); }
 
 // ------------------------------------------------------------ thread pool
 ThreadPool::ThreadPool(int n) {
@@ -564,6 +570,39 @@ void NodeIndex::update(const Address& block, const std::vector<Address>& old_h,
   }
 }
 
+void NodeIndex::update_many(const std::vector<Change>& changes) {
+  auto has = [](const std::vector<Address>& v, const Address& x) {
+    return std::find(v.begin(), v.end(), x) != v.end();
+  };
+  // (holder, block, add?) per stripe
+  std::array<std::vector<std::tuple<const Address*, const Address*, bool>>, kStripes> ops;
+  for (const Change& c : changes) {
+    for (size_t i = 0; i < c.old_h.size(); ++i) {
+      const Address& h = c.old_h[i];
+      if (!h || has(c.new_h, h) || std::find(c.old_h.begin(), c.old_h.begin() + i, h) != c.old_h.begin() + i)
+        continue;
+      ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, false);
+    }
+    for (const Address& h : c.new_h)
+      if (h && !has(c.old_h, h)) ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
+  }
+  for (size_t si = 0; si < kStripes; ++si) {
+    if (ops[si].empty()) continue;
+    Stripe& s = st_[si];
+    std::lock_guard<std::mutex> g(s.mu);
+    for (auto& [h, b, add] : ops[si]) {
+      if (add) {
+        s.m[*h].insert(*b);
+      } else {
+        auto it = s.m.find(*h);
+        if (it == s.m.end()) continue;
+        it->second.erase(*b);
+        if (it->second.empty()) s.m.erase(it);
+      }
+    }
+  }
+}
+
 std::vector<Address> NodeIndex::blocks(const Address& node) const {
   Stripe& s = stripe(node);
   std::lock_guard<std::mutex> g(s.mu);
@@ -633,7 +672,7 @@ void ErasureConsensus::batcher_loop() {
 
 // Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360).
 void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstride,
-                             const uint8_t* data, size_t dstride, bool parallel) {
+                             const uint8_t* data, size_t dstride, bool parallel, Placed* defer) {
   const int total = o_.k + o_.m;
   const size_t S = memo_ec_shard_size(b.data.size(), o_.k);
   Buffer own;
@@ -652,11 +691,12 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
   pl.owner = b.owner;
   pl.holder.assign(total, Address());
   std::vector<int> ok(total, 0);
+  const ShardKeys keys(b.address);
   auto put = [&](size_t i) {
     const ShardHeader h = header_of(b.address, pl, (int)i);
     const uint8_t* p = i < (size_t)o_.k ? data + i * dstride : parity + (i - o_.k) * pstride;
     try {
-      owners[i]->store(shard_key(b.address, (int)i), encode_shard(h, p));
+      owners[i]->store(keys((int)i), encode_shard(h, p));
       ok[i] = 1;
     } catch (Unavailable&) {
     }
@@ -670,17 +710,40 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
       pl.holder[i] = owners[i]->id;
       ++reached;
     }
-  const std::vector<Address> holders = pl.holder;
-  std::vector<Address> old;
-  {
-    std::unique_lock<std::shared_mutex> g(index_mu_);
-    old = swap_placement_locked(b.address, std::move(pl));
+  if (defer) {
+    defer->a = b.address;
+    defer->pl = std::move(pl);
+    defer->set = true;
+  } else {
+    const std::vector<Address> holders = pl.holder;
+    std::vector<Address> old;
+    {
+      std::unique_lock<std::shared_mutex> g(index_mu_);
+      old = swap_placement_locked(b.address, std::move(pl));
+    }
+    nodes_.update(b.address, old, holders);
   }
-  nodes_.update(b.address, old, holders);
   if (reached < o_.k)
     throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
                       std::to_string(o_.k));
   ++stored_;
+}
+
+void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
+  std::vector<NodeIndex::Change> ch;
+  ch.reserve(placed.size());
+  {
+    std::unique_lock<std::shared_mutex> g(index_mu_);
+    for (Placed& p : placed) {
+      if (!p.set) continue;
+      NodeIndex::Change c;
+      c.block = p.a;
+      c.new_h = p.pl.holder;
+      c.old_h = swap_placement_locked(p.a, std::move(p.pl));
+      ch.push_back(std::move(c));
+    }
+  }
+  nodes_.update_many(ch);
 }
 
 void ErasureConsensus::_store(const Block& b, StoreMode mode) {
@@ -736,11 +799,22 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
       tm.lap("encode");
       // shards straight from the batch buffers (a block's shard is the first
       // Sb bytes of its S-byte slot)
-      pool_.parallel_for(n, [&](size_t i) {
-        place(*g.second[i], parity.data() + i * o_.m * S, S, data.data() + i * o_.k * S, S,
-              /*parallel=*/false);  // already on the pool
-      });
+      // the shards go out on the pool; the batch's placements then enter
+      // the index under one lock (also when some block fell short)
+      std::vector<Placed> placed(n);
+      std::exception_ptr err;
+      try {
+        pool_.parallel_for(n, [&](size_t i) {
+          place(*g.second[i], parity.data() + i * o_.m * S, S, data.data() + i * o_.k * S, S,
+                /*parallel=*/false, &placed[i]);  // already on the pool
+        });
+      } catch (...) {
+        err = std::current_exception();
+      }
       tm.lap("place");
+      commit_placements(placed);
+      tm.lap("index");
+      if (err) std::rethrow_exception(err);
     }
   }
 }
@@ -759,13 +833,12 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
                                                                     ShardHeader* hdr,
                                                                     bool parallel) {
   const int total = o_.k + o_.m;
-  // shard keys (a SHA-256 each) are derived when a pass first needs them,
-  // always outside the parallel fetches: the data shards' first
+  // the shard keys (one SHA-256 for the block), outside the parallel fetches
   std::vector<Key> keys(total);
-  int keyed = 0;
-  auto key_upto = [&](int n) {
-    for (; keyed < n; ++keyed) keys[keyed] = shard_key(a, keyed);
-  };
+  {
+    const ShardKeys sk(a);
+    for (int i = 0; i < total; ++i) keys[i] = sk(i);
+  }
   std::map<int, Buffer> got;
   std::mutex gm;
   bool have_ref = false;
@@ -824,7 +897,6 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
   for (int pass = 0; pass < 2 && count() < want; ++pass) {
     // pass 0: the data shards (no decode needed); pass 1: the parity shards
-    key_upto(pass ? total : o_.k);
     std::vector<int> ids;
     for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i)
       if (holder[i] && !holder[i]->evicted && !have(i)) ids.push_back(i);
@@ -832,7 +904,6 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
 
   if (count() < want) {
-    key_upto(total);
     auto nodes = overlay_.lookup(a, (int)overlay_.size());
     auto from_node = [&](const std::shared_ptr<Node>& nd) {
       for (int i = 0; i < total; ++i)
@@ -1039,10 +1110,11 @@ void ErasureConsensus::_remove(const Address& a) {
     }
     nodes_.update(a, old, {});
   }
+  const ShardKeys keys(a);
   for (auto& nd : overlay_.lookup(a, (int)overlay_.size()))
     for (int i = 0; i < o_.k + o_.m; ++i) {
       try {
-        nd->remove(shard_key(a, i));
+        nd->remove(keys(i));
       } catch (Error&) {
       }
     }
@@ -1100,6 +1172,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         x.pl = it->second;
       }
       const ShardHeader ref = header_of(x.a, x.pl, 0);
+      const ShardKeys keys(x.a);
       for (int i = 0; i < total; ++i) {
         const Address& o = i < (int)x.pl.holder.size() ? x.pl.holder[i] : Address();
         auto nd = o ? overlay_.node(o) : nullptr;
@@ -1108,7 +1181,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           continue;
         }
         if (!nd->up) continue;  // unreachable for now: neither lost nor usable
-        const Key key = shard_key(x.a, i);
+        const Key key = keys(i);
         if ((int)x.surv.size() < k) {
           Buffer w;
           bool ok = false;
@@ -1203,6 +1276,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
             if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
               taken.insert(x.pl.holder[i]);
           auto cand = overlay_.allocate(x.a, (int)overlay_.size());
+          const ShardKeys keys(x.a);
           size_t ci = 0;
           for (int r = 0; r < e; ++r) {
             const int i = x.lost[r];
@@ -1213,7 +1287,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
               auto& nd = cand[ci++];
               if (taken.count(nd->id)) continue;
               try {
-                nd->store(shard_key(x.a, i), wire);
+                nd->store(keys(i), wire);
                 x.pl.holder[i] = nd->id;
                 taken.insert(nd->id);
                 ++placed[bi];
@@ -1225,7 +1299,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
               auto on = overlay_.node(old);
               if (on && on->up && !on->evicted) {
                 try {
-                  on->remove(shard_key(x.a, i));
+                  on->remove(keys(i));
                 } catch (Error&) {
                 }
               }

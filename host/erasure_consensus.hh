@@ -159,7 +159,15 @@ ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
 // checked, the checksum cannot be (it covers the payload).  Index rescans
 // use it; fetch and repair validate whole shards.
 ShardHeader decode_shard_header(const uint8_t* wire, size_t n);
-// Silo key of shard `index` of block `address`.
+// Silo keys of the shards of block `address`: one SHA-256 of (address,
+// tag) per block, shard i's key that hash with i folded into its first
+// byte (keys of one block are distinct; the flag byte marks them immutable).
+struct ShardKeys {
+  std::array<uint8_t, 32> base;
+  explicit ShardKeys(const Address& address);
+  Key operator()(int index) const;
+};
+// Silo key of shard `index` of block `address` (ShardKeys(address)(index)).
 Key shard_key(const Address& address, int index);
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
 
@@ -192,6 +200,12 @@ class NodeIndex {
   // old holders -> new holders of `block` (null addresses ignored)
   void update(const Address& block, const std::vector<Address>& old_h,
               const std::vector<Address>& new_h);
+  struct Change {
+    Address block;
+    std::vector<Address> old_h, new_h;
+  };
+  // update() for many blocks, each stripe locked once
+  void update_many(const std::vector<Change>& changes);
   std::vector<Address> blocks(const Address& node) const;
   size_t count(const Address& node) const;
 
@@ -283,6 +297,11 @@ class ErasureConsensus : public StackedConsensus {
     Address owner;                // CHB owner
     std::vector<Address> holder;  // node holding shard i (null: unplaced)
   };
+  struct Placed {
+    Address a;
+    Placement pl;
+    bool set = false;
+  };
   struct EncodeJob {
     const Block* block;
     std::promise<Buffer> parity;  // m x S
@@ -304,8 +323,12 @@ class ErasureConsensus : public StackedConsensus {
   // parallel = false stores the shards one by one (callers on the pool).
   // Shard i of b to owner i: data shard j at data + j*dstride (nullptr: b's
   // own zero-padded payload), parity shard r at parity + r*pstride.
+  // defer: the placement is left in *defer for commit_placements (a batch
+  // of blocks then takes the index lock once) instead of recorded here.
+  struct Placed;
   void place(const Block& b, const uint8_t* parity, size_t pstride, const uint8_t* data,
-             size_t dstride, bool parallel = true);
+             size_t dstride, bool parallel = true, Placed* defer = nullptr);
+  void commit_placements(std::vector<Placed>& placed);
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);

@@ -189,9 +189,13 @@ int MemorySilo::_erase(const Key& k) {
 }
 
 std::vector<Key> MemorySilo::_list() {
-  std::lock_guard<std::mutex> g(mu_);
   std::vector<Key> out;
-  for (auto& kv : blocks_) out.push_back(kv.first);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    out.reserve(blocks_.size());
+    for (auto& kv : blocks_) out.push_back(kv.first);
+  }
+  std::sort(out.begin(), out.end());  // a deterministic order, as before
   return out;
 }
 
@@ -341,14 +345,31 @@ bool Node::try_fetch(const Key& k, Buffer& out) const {
 
 bool Node::has(const Key& k) const { return silo->contains(k); }
 
+namespace {
+// A handle that does not own the node (the overlay does): copying it touches
+// no reference count.
+std::shared_ptr<Node> handle(Node* n) { return n ? std::shared_ptr<Node>(std::shared_ptr<Node>(), n) : nullptr; }
+}  // namespace
+
+Overlay::Overlay() {
+  snaps_.push_back(std::make_unique<Snapshot>());
+  snap_.store(snaps_.back().get(), std::memory_order_release);
+}
+
+Overlay::~Overlay() = default;
+
 std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo> silo) {
   auto n = std::make_shared<Node>();
   n->id = id;
   n->silo = std::move(silo);
   {
-    std::unique_lock<std::shared_mutex> g(mu_);
-    nodes_.push_back(n);
-    by_id_[n->id] = n;
+    std::lock_guard<std::mutex> g(mu_);
+    auto next = std::make_unique<Snapshot>(*snap());
+    next->nodes.push_back(n.get());
+    next->by_id[n->id] = n.get();
+    owned_.push_back(n);
+    snaps_.push_back(std::move(next));
+    snap_.store(snaps_.back().get(), std::memory_order_release);
   }
   notify([](const Handlers& h) -> const NodeEvent& { return h.discovered; }, id);
   return n;
@@ -374,20 +395,20 @@ void Overlay::set_up(const Address& id, bool up) {
 }
 
 std::shared_ptr<Node> Overlay::node(const Address& id) const {
-  std::shared_lock<std::shared_mutex> g(mu_);
-  auto it = by_id_.find(id);
-  return it == by_id_.end() ? nullptr : it->second;
+  const Snapshot* s = snap();
+  auto it = s->by_id.find(id);
+  return it == s->by_id.end() ? nullptr : handle(it->second);
 }
 
 std::vector<std::shared_ptr<Node>> Overlay::nodes() const {
-  std::shared_lock<std::shared_mutex> g(mu_);
-  return nodes_;
+  const Snapshot* s = snap();
+  std::vector<std::shared_ptr<Node>> out;
+  out.reserve(s->nodes.size());
+  for (Node* n : s->nodes) out.push_back(handle(n));
+  return out;
 }
 
-size_t Overlay::size() const {
-  std::shared_lock<std::shared_mutex> g(mu_);
-  return nodes_.size();
-}
+size_t Overlay::size() const { return snap()->nodes.size(); }
 
 namespace {
 // Rendezvous score of (address, node): a 64-bit mix of both ids (the ids are
@@ -407,14 +428,15 @@ uint64_t rendezvous(const Address& a, const Address& n) {
 }  // namespace
 
 std::vector<std::shared_ptr<Node>> Overlay::rank(const Address& address) const {
-  auto all = nodes();
-  std::vector<std::pair<uint64_t, std::shared_ptr<Node>>> scored;
-  scored.reserve(all.size());
-  for (auto& n : all) scored.push_back({rendezvous(address, n->id), n});
+  const Snapshot* sn = snap();
+  std::vector<std::pair<uint64_t, Node*>> scored;
+  scored.reserve(sn->nodes.size());
+  for (Node* n : sn->nodes) scored.push_back({rendezvous(address, n->id), n});
   std::sort(scored.begin(), scored.end(),
             [](const auto& a, const auto& b) { return a.first < b.first; });
   std::vector<std::shared_ptr<Node>> out;
-  for (auto& s : scored) out.push_back(s.second);
+  out.reserve(scored.size());
+  for (auto& s : scored) out.push_back(handle(s.second));
   return out;
 }
 

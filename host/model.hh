@@ -182,7 +182,8 @@ class MemorySilo : public Silo {
   // Values are immutable once stored: readers take a reference under the
   // lock and copy outside it, writers copy before taking it.
   mutable std::mutex mu_;
-  std::map<Key, std::shared_ptr<const Buffer>> blocks_;
+  // hashed, as the reference's Memory silo (src/memo/silo/Memory.hh:15)
+  std::unordered_map<Key, std::shared_ptr<const Buffer>, AddressHash> blocks_;
 };
 
 // silo::Filesystem (src/memo/silo/Filesystem.cc:27-147): one file per key,
@@ -263,11 +264,26 @@ class Overlay {
   std::vector<std::shared_ptr<Node>> nodes() const;
   size_t size() const;
 
+  Overlay();
+  ~Overlay();
+  Overlay(const Overlay&) = delete;
+  Overlay& operator=(const Overlay&) = delete;
+
  private:
-  // read-mostly: lookups take the lock shared (many fetch threads at once)
-  mutable std::shared_mutex mu_;
-  std::vector<std::shared_ptr<Node>> nodes_;
-  std::unordered_map<Address, std::shared_ptr<Node>, AddressHash> by_id_;
+  // Nodes are only ever added (a node that leaves is marked down or
+  // evicted), so the membership is an immutable snapshot replaced on each
+  // add: lookups read it with one atomic load -- no lock, no shared
+  // reference count touched by the many fetch/store threads -- and hand out
+  // non-owning handles to nodes the overlay keeps alive for its lifetime.
+  struct Snapshot {
+    std::vector<Node*> nodes;
+    std::unordered_map<Address, Node*, AddressHash> by_id;
+  };
+  const Snapshot* snap() const { return snap_.load(std::memory_order_acquire); }
+  std::mutex mu_;                                  // writers (add_node)
+  std::vector<std::shared_ptr<Node>> owned_;       // every node ever added
+  std::vector<std::unique_ptr<Snapshot>> snaps_;   // every snapshot (kept: readers may hold one)
+  std::atomic<const Snapshot*> snap_{nullptr};
   // Handlers run under hmu_: once unsubscribe() returns, none of that
   // subscriber's handlers is running or will run.
   std::mutex hmu_;

@@ -71,6 +71,8 @@ int main(int argc, char** argv) {
   ErasureOptions o;
   o.k = k;
   o.m = m;
+  // MEMO_EC_PLUGIN_THREADS: host pool size (scaling runs)
+  if (const char* t = std::getenv("MEMO_EC_PLUGIN_THREADS")) o.threads = std::atoi(t);
   ErasureConsensus ec(std::make_unique<ReplicationConsensus>(en.overlay, factor), en.overlay, o);
   // The first half of the blocks is stored cold (the codec contexts allocate
   // their pinned and device scratch on first use), the second half warm;
