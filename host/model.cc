@@ -133,16 +133,18 @@ bool Silo::_contains(const Key& k) const {
 }
 
 bool MemorySilo::_contains(const Key& k) const {
-  std::lock_guard<std::mutex> g(mu_);
-  return blocks_.count(k) != 0;
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  return st.blocks.count(k) != 0;
 }
 
 bool MemorySilo::_try_get(const Key& k, Buffer& out) const {
   std::shared_ptr<const Buffer> v;
   {
-    std::lock_guard<std::mutex> g(mu_);
-    auto it = blocks_.find(k);
-    if (it == blocks_.end()) return false;
+    Stripe& st = stripe(k);
+    std::lock_guard<std::mutex> g(st.mu);
+    auto it = st.blocks.find(k);
+    if (it == st.blocks.end()) return false;
     v = it->second;
   }
   out = *v;
@@ -152,9 +154,10 @@ bool MemorySilo::_try_get(const Key& k, Buffer& out) const {
 Buffer MemorySilo::_get(const Key& k) const {
   std::shared_ptr<const Buffer> v;
   {
-    std::lock_guard<std::mutex> g(mu_);
-    auto it = blocks_.find(k);
-    if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
+    Stripe& st = stripe(k);
+    std::lock_guard<std::mutex> g(st.mu);
+    auto it = st.blocks.find(k);
+    if (it == st.blocks.end()) throw silo::MissingKey("missing key " + k.hex());
     v = it->second;
   }
   return *v;
@@ -163,11 +166,12 @@ Buffer MemorySilo::_get(const Key& k) const {
 int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
   auto nv = std::make_shared<const Buffer>(v);  // the copy, outside the lock
   std::shared_ptr<const Buffer> old;            // freed outside the lock
-  std::lock_guard<std::mutex> g(mu_);
-  auto it = blocks_.find(k);
-  if (it == blocks_.end()) {
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  auto it = st.blocks.find(k);
+  if (it == st.blocks.end()) {
     if (!insert) throw silo::MissingKey("missing key " + k.hex());
-    blocks_.emplace(k, std::move(nv));
+    st.blocks.emplace(k, std::move(nv));
     return (int)v.size();
   }
   if (!update) throw silo::Collision("key exists " + k.hex());
@@ -179,23 +183,23 @@ int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
 
 int MemorySilo::_erase(const Key& k) {
   std::shared_ptr<const Buffer> old;
-  std::lock_guard<std::mutex> g(mu_);
-  auto it = blocks_.find(k);
-  if (it == blocks_.end()) throw silo::MissingKey("missing key " + k.hex());
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  auto it = st.blocks.find(k);
+  if (it == st.blocks.end()) throw silo::MissingKey("missing key " + k.hex());
   const int delta = -(int)it->second->size();
   old = std::move(it->second);
-  blocks_.erase(it);
+  st.blocks.erase(it);
   return delta;
 }
 
 std::vector<Key> MemorySilo::_list() {
   std::vector<Key> out;
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    out.reserve(blocks_.size());
-    for (auto& kv : blocks_) out.push_back(kv.first);
+  for (auto& st : st_) {
+    std::lock_guard<std::mutex> g(st.mu);
+    for (auto& kv : st.blocks) out.push_back(kv.first);
   }
-  std::sort(out.begin(), out.end());  // a deterministic order, as before
+  std::sort(out.begin(), out.end());  // a deterministic order
   return out;
 }
 

@@ -180,10 +180,17 @@ class MemorySilo : public Silo {
 
  private:
   // Values are immutable once stored: readers take a reference under the
-  // lock and copy outside it, writers copy before taking it.
-  mutable std::mutex mu_;
-  // hashed, as the reference's Memory silo (src/memo/silo/Memory.hh:15)
-  std::unordered_map<Key, std::shared_ptr<const Buffer>, AddressHash> blocks_;
+  // lock and copy outside it, writers copy before taking it.  Hashed, as
+  // the reference's Memory silo (src/memo/silo/Memory.hh:15), in stripes
+  // with a lock each (the reference's silo serves one reactor thread; this
+  // one serves a pool).
+  struct Stripe {
+    mutable std::mutex mu;
+    std::unordered_map<Key, std::shared_ptr<const Buffer>, AddressHash> blocks;
+  };
+  static constexpr size_t kStripes = 16;
+  Stripe& stripe(const Key& k) const { return st_[(AddressHash()(k) >> 56) % kStripes]; }
+  mutable std::array<Stripe, kStripes> st_;
 };
 
 // silo::Filesystem (src/memo/silo/Filesystem.cc:27-147): one file per key,
