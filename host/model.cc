@@ -106,6 +106,14 @@ int Silo::set(const Key& k, const Buffer& v, bool insert, bool update) {
   return delta;
 }
 
+int Silo::set(const Key& k, Buffer&& v, bool insert, bool update) {
+  if (capacity_ >= 0 && usage_ + (int64_t)v.size() > capacity_)
+    throw silo::InsufficientSpace("insufficient space");
+  const int delta = _set_moved(k, std::move(v), insert, update);
+  usage_ += delta;
+  return delta;
+}
+
 int Silo::erase(const Key& k) {
   const int delta = _erase(k);
   usage_ += delta;
@@ -164,18 +172,26 @@ Buffer MemorySilo::_get(const Key& k) const {
 }
 
 int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
-  auto nv = std::make_shared<const Buffer>(v);  // the copy, outside the lock
-  std::shared_ptr<const Buffer> old;            // freed outside the lock
+  return put(k, std::make_shared<const Buffer>(v), insert, update);  // the copy, outside the lock
+}
+
+int MemorySilo::_set_moved(const Key& k, Buffer&& v, bool insert, bool update) {
+  return put(k, std::make_shared<const Buffer>(std::move(v)), insert, update);
+}
+
+int MemorySilo::put(const Key& k, std::shared_ptr<const Buffer> nv, bool insert, bool update) {
+  std::shared_ptr<const Buffer> old;  // freed outside the lock
+  const int size = (int)nv->size();
   Stripe& st = stripe(k);
   std::lock_guard<std::mutex> g(st.mu);
   auto it = st.blocks.find(k);
   if (it == st.blocks.end()) {
     if (!insert) throw silo::MissingKey("missing key " + k.hex());
     st.blocks.emplace(k, std::move(nv));
-    return (int)v.size();
+    return size;
   }
   if (!update) throw silo::Collision("key exists " + k.hex());
-  const int delta = (int)v.size() - (int)it->second->size();
+  const int delta = size - (int)it->second->size();
   old = std::move(it->second);
   it->second = std::move(nv);
   return delta;
@@ -327,6 +343,13 @@ void Node::store(const Key& k, const Buffer& v) {
   if (!up || evicted) throw Unavailable("node down");
   if (fail_stores) throw Unavailable("store refused");
   silo->set(k, v, true, true);
+  ++stores;
+}
+
+void Node::store(const Key& k, Buffer&& v) {
+  if (!up || evicted) throw Unavailable("node down");
+  if (fail_stores) throw Unavailable("store refused");
+  silo->set(k, std::move(v), true, true);
   ++stores;
 }
 

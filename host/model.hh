@@ -146,6 +146,8 @@ class Silo {
   bool contains(const Key& k) const { return _contains(k); }
   // insert: accept a new key; update: accept an existing key.
   int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
+  // set() of a value the caller gives up (a silo may keep it without a copy)
+  int set(const Key& k, Buffer&& v, bool insert = true, bool update = false);
   int erase(const Key& k);
   std::vector<Key> list() { return _list(); }
   virtual std::string type() const = 0;
@@ -158,6 +160,7 @@ class Silo {
   virtual bool _contains(const Key& k) const;                // default: _try_get
   virtual bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const;  // default: _try_get
   virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
+  virtual int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) { return _set(k, v, insert, update); }
   virtual int _erase(const Key& k) = 0;
   virtual std::vector<Key> _list() = 0;
   int64_t capacity_;
@@ -175,10 +178,12 @@ class MemorySilo : public Silo {
   bool _try_get(const Key& k, Buffer& out) const override;
   bool _contains(const Key& k) const override;
   int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
+  int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) override;
   int _erase(const Key& k) override;
   std::vector<Key> _list() override;
 
  private:
+  int put(const Key& k, std::shared_ptr<const Buffer> nv, bool insert, bool update);
   // Values are immutable once stored: readers take a reference under the
   // lock and copy outside it, writers copy before taking it.  Hashed, as
   // the reference's Memory silo (src/memo/silo/Memory.hh:15), in stripes
@@ -232,6 +237,7 @@ struct Node {
   std::atomic<bool> fail_stores{false};
 
   void store(const Key& k, const Buffer& v);
+  void store(const Key& k, Buffer&& v);
   Buffer fetch(const Key& k) const;
   // fetch() that reports a missing key by returning false (no exception);
   // throws Unavailable when the node is down.
