@@ -898,14 +898,25 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   for (int pass = 0; pass < 2 && count() < want; ++pass) {
     // pass 0: the data shards (no decode needed); pass 1: the parity shards
     std::vector<int> ids;
-    for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i)
-      if (holder[i] && !holder[i]->evicted && !have(i)) ids.push_back(i);
+    for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i) {
+      if (!holder[i] || holder[i]->evicted || have(i)) continue;
+      if (!holder[i]->up) {  // known down: no fetch (and no exception) for it
+        any_down = true;
+        continue;
+      }
+      ids.push_back(i);
+    }
     run(ids.size(), [&](size_t t) { try_node(holder[ids[t]], ids[t]); });
   }
 
   if (count() < want) {
     auto nodes = overlay_.lookup(a, (int)overlay_.size());
     auto from_node = [&](const std::shared_ptr<Node>& nd) {
+      if (!nd->up) {
+        std::lock_guard<std::mutex> g(gm);
+        any_down = true;
+        return;
+      }
       for (int i = 0; i < total; ++i)
         if (!have(i) && !try_node(nd, i)) return;  // down: skip the node
     };
