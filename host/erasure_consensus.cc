@@ -577,14 +577,23 @@ void NodeIndex::update_many(const std::vector<Change>& changes) {
   // (holder, block, add?) per stripe
   std::array<std::vector<std::tuple<const Address*, const Address*, bool>>, kStripes> ops;
   for (const Change& c : changes) {
+    // holders that stayed in place need no membership test (a repair moves
+    // e of k + m)
+    auto same_at = [&](const std::vector<Address>& v, size_t i, const Address& h) {
+      return i < v.size() && v[i] == h;
+    };
     for (size_t i = 0; i < c.old_h.size(); ++i) {
       const Address& h = c.old_h[i];
-      if (!h || has(c.new_h, h) || std::find(c.old_h.begin(), c.old_h.begin() + i, h) != c.old_h.begin() + i)
+      if (!h || same_at(c.new_h, i, h) || has(c.new_h, h) ||
+          std::find(c.old_h.begin(), c.old_h.begin() + i, h) != c.old_h.begin() + i)
         continue;
       ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, false);
     }
-    for (const Address& h : c.new_h)
-      if (h && !has(c.old_h, h)) ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
+    for (size_t i = 0; i < c.new_h.size(); ++i) {
+      const Address& h = c.new_h[i];
+      if (h && !same_at(c.old_h, i, h) && !has(c.old_h, h))
+        ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
+    }
   }
   for (size_t si = 0; si < kStripes; ++si) {
     if (ops[si].empty()) continue;
@@ -1165,6 +1174,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
   }
   for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
     const size_t c0 = cuts[ci], cn = cuts[ci + 1] - c0;
+    PhaseTimer tm("repair_chunk");
     std::vector<Todo> todo(cn);
     // Scan: a shard is lost when its holder is gone (null, evicted, down
     // with include_down), lacks it, or holds a copy that fails validation
@@ -1212,6 +1222,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         }
       }
     });
+    tm.lap("scan");
     std::vector<Todo*> work;
     for (auto& x : todo) {
       if (x.skip || x.lost.empty()) continue;
@@ -1270,12 +1281,14 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           x.surv.clear();
           x.surv.shrink_to_fit();
         });
+        tm.lap("copy_in");
         if (grp.uniform)
           codec_.rebuild_uniform(k, m, S, n, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
                                  out.data(), pin);
         else
           codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data(), pin);
         ++rep.codec_calls;
+        tm.lap("rebuild");
         std::vector<int> placed(n, 0);
         // place each rebuilt shard on a reachable node holding none of the
         // block's other shards (Overlay::allocate order); the stale copy on
@@ -1317,17 +1330,31 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
             }
           }
         });
+        tm.lap("place");
+        // the batch's new placements enter the index under one lock
+        std::vector<char> gone(n, 0);
+        std::vector<NodeIndex::Change> ch;
+        ch.reserve(n);
+        {
+          std::unique_lock<std::shared_mutex> lk(index_mu_);
+          for (size_t bi = 0; bi < n; ++bi) {
+            Todo& x = *grp.items[b0 + bi];
+            if (!index_.count(x.a)) {
+              gone[bi] = 1;
+              continue;
+            }
+            NodeIndex::Change c;
+            c.block = x.a;
+            c.new_h = x.pl.holder;
+            c.old_h = swap_placement_locked(x.a, std::move(x.pl));  // x.pl unused from here
+            ch.push_back(std::move(c));
+          }
+        }
+        nodes_.update_many(ch);
+        tm.lap("index");
         for (size_t bi = 0; bi < n; ++bi) {
           Todo& x = *grp.items[b0 + bi];
-          bool removed = false;
-          std::vector<Address> old;
-          {
-            std::unique_lock<std::shared_mutex> lk(index_mu_);
-            if (index_.count(x.a)) old = swap_placement_locked(x.a, x.pl);
-            else removed = true;
-          }
-          if (!removed) nodes_.update(x.a, old, x.pl.holder);
-          if (removed) {  // removed while being repaired: drop the new shards
+          if (gone[bi]) {  // removed while being repaired: drop the new shards
             for (int i : x.lost)
               if (x.pl.holder[i])
                 if (auto nd = overlay_.node(x.pl.holder[i])) {
