@@ -190,22 +190,26 @@ def test_c1_full_size_vs_oracle(codec, O):
         assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), e
 
 
-@pytest.mark.parametrize("k,m", [(3, 2), (4, 2)])
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3), (10, 4), (12, 4), (16, 4)])
 def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
     """Each block of the batch has a different erasure pattern (per-block
-    decode tables in one launch); all patterns of size m."""
-    pats = list(itertools.combinations(range(k + m), m))
-    n, B = len(pats), 3000
-    S = O.shard_size(B, k)
-    data = O.fill_blocks(SEED, 0, n, B, k, S)
-    par = O.encode(k, m, S, data)
-    lost = np.array(pats, dtype=np.uint8)
-    surv = np.array([[i for i in range(k + m) if i not in p][:k] for p in pats], dtype=np.uint8)
-    sv = O.gather(k, m, S, data, par, surv)
-    out = empty(n, m * S)
-    codec.rebuild(k, m, dev(surv), dev(sv), dev(lost), out)
-    codec.synchronize()
-    assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost))
+    decode tables in one launch): for every e = 1..m, every set of e lost
+    shards of the code (C(k+m, e) blocks; RS(16,4): 20 + 190 + 1140 + 4845),
+    rebuilt from the first k survivors, against the oracle's gather of the
+    encoded shards."""
+    for e in range(1, m + 1):
+        pats = list(itertools.combinations(range(k + m), e))
+        n, B = len(pats), 3000 if k <= 4 else 1000
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, e, n, B, k, S)
+        par = O.encode(k, m, S, data)
+        lost = np.array(pats, dtype=np.uint8)
+        surv = np.array([[i for i in range(k + m) if i not in p][:k] for p in pats], dtype=np.uint8)
+        sv = O.gather(k, m, S, data, par, surv)
+        out = empty(n, e * S)
+        codec.rebuild(k, m, dev(surv), dev(sv), dev(lost), out)
+        codec.synchronize()
+        assert np.array_equal(host(out), O.gather(k, m, S, data, par, lost)), (k, m, e)
 
 
 @pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 2), (4, 2), (6, 3), (7, 5), (8, 8), (10, 4),
