@@ -155,6 +155,8 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
 // Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
 // payload length, CRC32C over header and payload); throws ValidationFailed.
 ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
+// *payload would point into a temporary that dies with the call.
+ShardHeader decode_shard(Buffer&& wire, const uint8_t** payload) = delete;
 // The header alone (the first kSize bytes): magic, version and geometry are
 // checked, the checksum cannot be (it covers the payload).  Index rescans
 // use it; fetch and repair validate whole shards.

@@ -588,7 +588,8 @@ TEST(owned_chb_round_trip_degraded, true) {
       const Key key = shard_key(b.address, i);
       if (!n->up || !n->has(key)) continue;
       const uint8_t* p = nullptr;
-      ShardHeader h = decode_shard(n->silo->get(key), &p);
+      const Buffer w = n->silo->get(key);  // p points into it
+      ShardHeader h = decode_shard(w, &p);
       h.owner = other;
       n->silo->set(key, encode_shard(h, p), false, true);
     }
