@@ -1118,6 +1118,8 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   for (size_t i = 0; i < n; ++i) res(addresses[i], std::move(blocks[i]), errs[i]);
 }
 
+void ErasureConsensus::_resign() { backend_->resign(); }
+
 void ErasureConsensus::_remove(const Address& a) {
   if (a.mutable_block()) return backend_->remove(a);
   {

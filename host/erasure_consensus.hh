@@ -291,6 +291,12 @@ class ErasureConsensus : public StackedConsensus {
   std::unique_ptr<Block> _fetch(const Address& a) override;
   void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) override;
   void _remove(const Address& a) override;
+  // Leaving the network: the mutable blocks' backend hands its blocks off
+  // (Paxos::_resign, Paxos.cc:2091-2131, which rebalances mutable blocks
+  // only); shards stay where they are, and the remaining nodes' eviction
+  // timers repair them once this node is gone, as for Paxos's immutable
+  // replicas.
+  void _resign() override;
 
  private:
   struct Placement {

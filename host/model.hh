@@ -332,6 +332,8 @@ class Consensus {
     _fetch(addresses, res);
   }
   void remove(const Address& a) { _remove(a); }
+  // Consensus::resign (Consensus.cc:167-176): the local node is leaving.
+  void resign() { _resign(); }
   // Consensus::redundancy / stats (Consensus.cc:350-357): JSON text.
   virtual std::string redundancy() const = 0;
   virtual std::string stats() const { return "{}"; }
@@ -343,6 +345,7 @@ class Consensus {
   // (Consensus::_fetch, Consensus.cc:108-124).
   virtual void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res);
   virtual void _remove(const Address& a) = 0;
+  virtual void _resign() {}  // Consensus::_resign: nothing by default
 };
 
 // consensus::StackedConsensus (Consensus.hh:129-142).

@@ -352,6 +352,42 @@ TEST(mutable_blocks_use_backend, true) {
   CHECK(net.ec->fetch(b.address)->data == bytes("foobar"));
 }
 
+// Consensus::resign (Consensus.cc:167-176): the plugin hands the leave to
+// its mutable-block backend (Paxos::_resign rebalances mutable blocks only,
+// Paxos.cc:2091-2131) and leaves its shards in place for the other nodes'
+// eviction timers.
+namespace {
+struct CountingBackend : ReplicationConsensus {
+  using ReplicationConsensus::ReplicationConsensus;
+  int resigned = 0;
+  void _resign() override { ++resigned; }
+};
+}  // namespace
+TEST(resign_forwards_to_backend, true) {
+  Overlay overlay;
+  for (int i = 0; i < 16; ++i) {
+    uint8_t id[32] = {0};
+    id[0] = (uint8_t)(i + 1);
+    id[1] = 0x52;
+    overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>());
+  }
+  auto backend = std::make_unique<CountingBackend>(overlay, 3);
+  CountingBackend* bk = backend.get();
+  ErasureOptions o;
+  o.k = 10;
+  o.m = 4;
+  ErasureConsensus ec(std::move(backend), overlay, o);
+  Block b = make_chb(random_bytes(100000, 77));
+  ec.store(b);
+  ec.resign();
+  CHECK(bk->resigned == 1);
+  int shards = 0;
+  for (auto& n : overlay.nodes())
+    for (int i = 0; i < 14; ++i) shards += n->has(shard_key(b.address, i)) ? 1 : 0;
+  CHECK(shards == 14);
+  CHECK(ec.fetch(b.address)->data == b.data);
+}
+
 // tests/consensus/paxos.cc:7-63 (availability_2/3), for k+m: reads survive
 // up to m unreachable owners, a data-shard loss is rebuilt on the GPU, and
 // more than m losses raise TooFewPeers.
