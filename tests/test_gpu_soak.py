@@ -44,7 +44,10 @@ def test_soak_mixed_calls_threads(O, monkeypatch):
 
     def empty(shape, where):
         if where == "device":
-            return torch.zeros(shape, dtype=torch.uint8, device="cuda")
+            # torch.empty launches nothing: a zero fill would run on torch's
+            # stream, unordered with the codec's (non-blocking) ctx stream,
+            # and could land after the kernel that writes the output
+            return torch.empty(shape, dtype=torch.uint8, device="cuda")
         return torch.zeros(shape, dtype=torch.uint8, pin_memory=(where == "pinned"))
 
     def work(t):
