@@ -432,7 +432,7 @@ void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
 
 // --------------------------------------------------------------- plugin
 namespace {
-enum MemberEvent { kDiscovered = 0, kDisappeared = 1, kAppeared = 2 };
+enum MemberEvent { kDiscovered = 0, kDisappeared = 1, kAppeared = 2, kUnderPlaced = 3 };
 }
 
 ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& overlay,
@@ -731,6 +731,7 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
       old = swap_placement_locked(b.address, std::move(pl));
     }
     nodes_.update(b.address, old, holders);
+    if (o_.auto_expand && reached >= o_.k && reached < total) post(kUnderPlaced, b.address);
   }
   if (reached < o_.k)
     throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
@@ -741,10 +742,14 @@ void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstri
 void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
   std::vector<NodeIndex::Change> ch;
   ch.reserve(placed.size());
+  std::vector<Address> under;  // stored (>= k shards) but on fewer than k+m owners
   {
     std::unique_lock<std::shared_mutex> g(index_mu_);
     for (Placed& p : placed) {
       if (!p.set) continue;
+      const int held = (int)std::count_if(p.pl.holder.begin(), p.pl.holder.end(),
+                                          [](const Address& h) { return (bool)h; });
+      if (held >= o_.k && held < o_.k + o_.m) under.push_back(p.a);
       NodeIndex::Change c;
       c.block = p.a;
       c.new_h = p.pl.holder;
@@ -753,6 +758,8 @@ void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
     }
   }
   nodes_.update_many(ch);
+  if (o_.auto_expand)
+    for (auto& a : under) post(kUnderPlaced, a);
 }
 
 void ErasureConsensus::_store(const Block& b, StoreMode mode) {
@@ -1371,7 +1378,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           rep.shards_rebuilt += (size_t)placed[bi];
           rep.shards_unplaced += (size_t)e - (size_t)placed[bi];
           ++repaired_;
-          if (rebalanced_) rebalanced_(x.a);
+          if (rebalanced_ && placed[bi]) rebalanced_(x.a);  // moved onto new owners
         }
       }
     }
@@ -1494,10 +1501,10 @@ void ErasureConsensus::membership_loop() {
   std::unique_lock<std::mutex> l(mmu_);
   while (!mstop_) {
     if (mq_.empty()) {
-      if (evict_at_.empty()) {
+      if (evict_at_.empty() && under_.empty()) {
         mcv_.wait(l);
       } else {
-        auto next = evict_at_.begin()->second;
+        auto next = under_.empty() ? clock::time_point::max() : under_at_;
         for (auto& kv : evict_at_) next = std::min(next, kv.second);
         if (clock::now() < next) mcv_.wait_until(l, next);
       }
@@ -1512,9 +1519,20 @@ void ErasureConsensus::membership_loop() {
           evict_at_[ev.second] = clock::now() + std::chrono::milliseconds(o_.eviction_delay_ms);
       } else if (ev.first == kAppeared) {
         evict_at_.erase(ev.second);
+      } else if (ev.first == kUnderPlaced) {
+        if (under_.empty()) under_at_ = clock::now();
+        under_.insert(ev.second);
+        under_backoff_ = std::chrono::milliseconds(10);
       } else {
         expand_now = expand_now || o_.auto_expand;
       }
+    }
+    // under-placed stores, retried with backoff (10 ms doubling to 10 s,
+    // as Paxos's resign loop backs off, Paxos.cc:2098)
+    std::vector<Address> retry;
+    if (!under_.empty() && clock::now() >= under_at_) {
+      retry.assign(under_.begin(), under_.end());
+      under_.clear();
     }
     std::vector<Address> due;
     const auto now = clock::now();
@@ -1526,8 +1544,29 @@ void ErasureConsensus::membership_loop() {
         ++it;
       }
     }
-    if (due.empty() && !expand_now) continue;
+    if (due.empty() && !expand_now && retry.empty()) continue;
     l.unlock();
+    std::vector<Address> again;
+    if (!retry.empty()) {
+      try {
+        repair_blocks(retry, false);
+      } catch (std::exception& e) {
+        std::fprintf(stderr, "erasure: rebalancing failed: %s\n", e.what());
+      }
+      // still short of k+m owners while some reachable node holds none of
+      // the block's shards: try again later; otherwise wait for a discovery
+      // (Paxos: _under_replicated when no new owner exists, Paxos.cc:1120-1124)
+      size_t reachable = 0;
+      for (auto& n : overlay_.nodes()) reachable += (n->up && !n->evicted) ? 1 : 0;
+      std::shared_lock<std::shared_mutex> g(index_mu_);
+      for (auto& a : retry) {
+        auto it = index_.find(a);
+        if (it == index_.end()) continue;  // removed
+        const size_t held = (size_t)std::count_if(it->second.holder.begin(), it->second.holder.end(),
+                                                  [](const Address& h) { return (bool)h; });
+        if (held < it->second.holder.size() && reachable > held) again.push_back(a);
+      }
+    }
     for (auto& id : due) {
       auto nd = overlay_.node(id);
       if (!nd || nd->up) continue;  // came back
@@ -1545,6 +1584,14 @@ void ErasureConsensus::membership_loop() {
       }
     }
     l.lock();
+    if (!again.empty()) {
+      const bool fresh = under_.empty();
+      under_.insert(again.begin(), again.end());
+      if (fresh) {
+        under_at_ = clock::now() + under_backoff_;
+        under_backoff_ = std::min(under_backoff_ * 2, std::chrono::milliseconds(10000));
+      }
+    }
   }
 }
 

@@ -24,6 +24,7 @@
 #include <deque>
 #include <functional>
 #include <future>
+#include <set>
 #include <thread>
 #include <unordered_set>
 
@@ -372,6 +373,12 @@ class ErasureConsensus : public StackedConsensus {
   std::condition_variable mcv_;
   std::deque<std::pair<int, Address>> mq_;
   std::map<Address, std::chrono::steady_clock::time_point> evict_at_;
+  // blocks stored on fewer than k+m owners, retried with backoff while a
+  // reachable node holds none of their shards (Paxos's _rebalancable queue
+  // after an under-replicated insert, Paxos.cc:1428-1438, 1089-1127)
+  std::set<Address> under_;
+  std::chrono::steady_clock::time_point under_at_{};
+  std::chrono::milliseconds under_backoff_{10};
   bool mstop_ = false;
   int sub_token_ = -1;
   std::thread mthread_;

@@ -529,20 +529,50 @@ TEST(evict_and_repair, true) {
   for (auto& b : blocks) CHECK(net.ec->fetch(b.address)->data == b.data);
 }
 
-// CHB_unavailable (doughnut.cc:2158-2176): an owner refusing the store
-// leaves the block under-sharded; repair completes it.
+// CHB_unavailable (doughnut.cc:2158-2176): an owner refusing the store (its
+// store barrier raises Unavailable) leaves the block on k+m-1 owners; once
+// the barrier opens, the background rebalancing of under-placed stores
+// (rebalance_auto_expand, Paxos.cc:1428-1438) places the missing shard on
+// it without any repair call.  Exactly k+m nodes: the refusing owner is the
+// only node that can take the shard, so the retries before the barrier
+// opens cannot place it elsewhere.
 TEST(CHB_unavailable, true) {
-  Net net(16, 10, 4);
+  Net net(14, 10, 4);
+  std::atomic<int> rebalanced{0};
+  net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
   Block b = make_chb(bytes("CHB_unavailable"));
   auto owners = net.overlay.allocate(b.address, 14);
   owners[2]->fail_stores = true;
   net.ec->store(b);
   CHECK(net.shards(b.address, 14) == 13);
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));  // retries meet the barrier
+  CHECK(rebalanced.load() == 0 && net.shards(b.address, 14) == 13);
   owners[2]->fail_stores = false;
-  owners[2]->evicted = true;
-  auto rep = net.ec->repair();
-  CHECK(rep.shards_rebuilt == 1);
+  CHECK(wait_for([&] { return rebalanced.load() > 0; }));
   CHECK(net.shards(b.address, 14) == 14);
+  CHECK(net.holders(b.address, 14) == 14);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// expand_new_block (doughnut.cc:1484-1512): a block written while some of
+// its owners refuse stores is rebalanced onto them once they accept, and then
+// survives the loss of m other owners.
+TEST(expand_new_block, true) {
+  Net net(14, 10, 4);
+  std::atomic<int> rebalanced{0};
+  net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
+  Block b = make_chb(random_bytes(300000, 1484));
+  auto owners = net.overlay.allocate(b.address, 14);
+  owners[6]->fail_stores = true;
+  owners[11]->fail_stores = true;
+  net.ec->store(b);
+  CHECK(net.shards(b.address, 14) == 12);
+  owners[6]->fail_stores = false;
+  owners[11]->fail_stores = false;
+  CHECK(wait_for([&] { return net.shards(b.address, 14) == 14; }));
+  CHECK(rebalanced.load() > 0);
+  CHECK(net.holders(b.address, 14) == 14);
+  for (int i : {0, 3, 8, 13}) owners[i]->up = false;  // m losses, none of them the late owners
   CHECK(net.ec->fetch(b.address)->data == b.data);
 }
 
