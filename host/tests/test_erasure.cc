@@ -554,6 +554,37 @@ TEST(CHB_unavailable, true) {
   CHECK(net.ec->fetch(b.address)->data == b.data);
 }
 
+// evict_faulty (doughnut.cc:1651-1691): a block stored on all k+m nodes; a
+// newcomer joins; one owner disconnects and is evicted explicitly (the
+// reference calls Local::evict() on the survivors) -> its shard is rebuilt on
+// the newcomer, the only node without one, and the block then survives m
+// further losses.
+TEST(evict_faulty, true) {
+  Net net(14, 10, 4);
+  std::atomic<int> rebalanced{0};
+  net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
+  Block b = make_chb(random_bytes(200000, 1651));
+  net.ec->store(b);
+  CHECK(net.holders(b.address, 14) == 14);
+  auto d = net.add();  // fourth DHT: a discovery, nothing under-placed
+  std::shared_ptr<Node> faulty;
+  for (auto& n : net.nodes)
+    if (n != d && n->has(shard_key(b.address, 5))) faulty = n;
+  CHECK(faulty != nullptr);
+  faulty->up = false;  // disconnect third DHT
+  auto rep = net.ec->evict(faulty->id);
+  CHECK(rep.blocks_repaired == 1 && rep.shards_rebuilt == 1 && rep.unrecoverable == 0);
+  CHECK(rebalanced.load() == 1);
+  CHECK(d->has(shard_key(b.address, 5)));
+  int down = 0;  // disconnect first DHT (and m - 1 more owners)
+  for (auto& n : net.nodes)
+    if (n != d && n != faulty && down < 4) {
+      n->up = false;
+      ++down;
+    }
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
 // expand_new_block (doughnut.cc:1484-1512): a block written while some of
 // its owners refuse stores is rebalanced onto them once they accept, and then
 // survives the loss of m other owners.
