@@ -1548,23 +1548,33 @@ void ErasureConsensus::membership_loop() {
     l.unlock();
     std::vector<Address> again;
     if (!retry.empty()) {
-      try {
-        repair_blocks(retry, false);
-      } catch (std::exception& e) {
-        std::fprintf(stderr, "erasure: rebalancing failed: %s\n", e.what());
-      }
-      // still short of k+m owners while some reachable node holds none of
-      // the block's shards: try again later; otherwise wait for a discovery
-      // (Paxos: _under_replicated when no new owner exists, Paxos.cc:1120-1124)
-      size_t reachable = 0;
-      for (auto& n : overlay_.nodes()) reachable += (n->up && !n->evicted) ? 1 : 0;
-      std::shared_lock<std::shared_mutex> g(index_mu_);
-      for (auto& a : retry) {
-        auto it = index_.find(a);
-        if (it == index_.end()) continue;  // removed
-        const size_t held = (size_t)std::count_if(it->second.holder.begin(), it->second.holder.end(),
-                                                  [](const Address& h) { return (bool)h; });
-        if (held < it->second.holder.size() && reachable > held) again.push_back(a);
+      // Only blocks still short of k+m owners while some reachable node holds
+      // none of their shards are worth a rebuild; the others wait for a
+      // discovery (Paxos: _under_replicated when no new owner exists,
+      // Paxos.cc:1120-1124), so a network smaller than k+m does not decode
+      // every store's missing shards for nothing.
+      auto placeable = [&](const std::vector<Address>& v) {
+        size_t reachable = 0;
+        for (auto& n : overlay_.nodes()) reachable += (n->up && !n->evicted) ? 1 : 0;
+        std::vector<Address> out;
+        std::shared_lock<std::shared_mutex> g(index_mu_);
+        for (auto& a : v) {
+          auto it = index_.find(a);
+          if (it == index_.end()) continue;  // removed
+          const size_t held = (size_t)std::count_if(it->second.holder.begin(), it->second.holder.end(),
+                                                    [](const Address& h) { return (bool)h; });
+          if (held < it->second.holder.size() && reachable > held) out.push_back(a);
+        }
+        return out;
+      };
+      const std::vector<Address> todo = placeable(retry);
+      if (!todo.empty()) {
+        try {
+          repair_blocks(todo, false);
+        } catch (std::exception& e) {
+          std::fprintf(stderr, "erasure: rebalancing failed: %s\n", e.what());
+        }
+        again = placeable(todo);  // e.g. the candidate refused: try again later
       }
     }
     for (auto& id : due) {
