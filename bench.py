@@ -24,11 +24,17 @@ Printed JSON line (rank 0): the contract fields plus
   encode / rebuild : per-direction GiB/s, kernel ms and roofline fraction
   roofline         : the encode kernel (C2, the north-star target): its
                      algorithmic bytes per launch (k+m)*S*n / its average
-                     HIP-event duration, vs 8 TB/s; roofline_rebuild likewise
+                     HIP-event duration, vs 8 TB/s; roofline_rebuild likewise;
+                     `traffic` from rocprofv3 counter passes this run makes
+                     (pmc_traffic)
   ranks            : per-GPU GiB/s, node sum (C4's wording)
   cpu_baseline     : the C port (oracle/, test infrastructure) timed on this
-                     host's cores on a bounded sample (rank 0, N=1 only)
-  end_to_end       : pinned host -> HBM -> host rate (PCIe-inclusive; not `value`)
+                     host's CPU share on a bounded sample (rank 0, every N,
+                     after the timed steps)
+  end_to_end       : pinned host -> HBM -> host rate (PCIe-inclusive; not
+                     `value`), every rank over its own link, node sum at N>1
+  build_id         : memo_ec_build_id() of the loaded library (== SHA-256 of
+                     the sources in this tree: build_matches_sources)
 """
 import argparse
 import json
@@ -63,6 +69,8 @@ def parse(argv=None):
     ap.add_argument("--no-small", action="store_true", help="skip the 4 KiB random-rebuild lines")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the rocprofv3 FETCH_SIZE / WRITE_SIZE passes behind roofline.traffic")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--sweep", action="store_true", help="also run the C5 mixed sweep")
     ap.add_argument("--sha", action="store_true",
@@ -119,10 +127,26 @@ def kstats(kms, alg_bytes):
 
 def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
     """BASELINE.json C5: (k,m) in {(4,2),(10,4),(16,4)} x B in 4 KiB..4 MiB,
-    ~gib GiB of payload per point, one encode launch per step; then the same
-    12 smaller groups as ONE memo_ec_encode_segments call (one launch per
-    shard-chunk class, back to back; timed from before the first launch to
-    after the last)."""
+    ~gib GiB of payload per point.  Each point times one encode launch and
+    one rebuild of the same blocks with e = m random erasures per block (the
+    metric is encode+rebuild), both checked bit-exact on the GPU.  Then the
+    same 12 smaller groups as ONE memo_ec_encode_segments call and ONE
+    memo_ec_rebuild_segments call (one launch per shard-chunk class, back to
+    back; timed from before the first launch to after the last)."""
+    def frac(alg, ms):
+        return round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+
+    def rebuild_inputs(k, m, S, n, d, p, fb=0):
+        e = m
+        s_idx, l_idx = ec.erasures(SEED, fb, n, k, m, e)
+        sd, ld = torch.from_numpy(s_idx).cuda(), torch.from_numpy(l_idx).cuda()
+        surv = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        codec.gather_shards(k, m, S, n, d, p, ld, want)
+        out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+        return e, s_idx, l_idx, sd, ld, surv, want, out
+
     points = []
     for (k, m) in [(4, 2), (10, 4), (16, 4)]:
         for B in [4 << 10, 16 << 10, 64 << 10, 256 << 10, 1 << 20, 4 << 20]:
@@ -131,50 +155,77 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
             p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
             codec.fill_blocks(SEED, 0, n, B, k, S, d)
-            _, (kms,), _ = timed_steps(torch, [lambda: codec.encode(k, m, d, p)], steps, warmup,
-                                       settle_ms, None, stream)
-            ms = float(np.mean(kms))
-            alg = (k + m) * S * n
+            codec.encode(k, m, d, p)
+            e, s_idx, l_idx, sd, ld, surv, want, out = rebuild_inputs(k, m, S, n, d, p)
+            _, (kms, rms), _ = timed_steps(
+                torch, [lambda: codec.encode(k, m, d, p), lambda: codec.rebuild(k, m, sd, surv, ld, out)],
+                steps, warmup, settle_ms, None, stream)
+            codec.synchronize()
+            ms, rs = float(np.mean(kms)), float(np.mean(rms))
             pt = {"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
                   "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
-                  "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+                  "frac": frac((k + m) * S * n, ms),
+                  "rebuild": {"erasures": e, "kernel": ec.rebuild_path(n, k, S), "step_ms": round(rs, 4),
+                              "GiBs": round(n * B / (rs * 1e-3) / 2**30, 1),
+                              "frac": frac((k + e) * S * n, rs),
+                              "bit_exact": bool(torch.equal(out, want))},
+                  "encode_rebuild_GiBs": round(2 * n * B / ((ms + rs) * 1e-3) / 2**30, 1)}
             if cpu:
                 # CPU baseline of the point (per C5 point): the
-                # vectorised port on 16 threads over a ~64 MiB sample of the blocks
+                # vectorised port on 16 threads over a ~64 MiB sample of the
+                # blocks, encode and the same blocks' rebuild
                 from oracle import oracle as O
                 nc = max(16, min(n, (64 << 20) // B))
                 hd = O.aligned_empty((nc, k * S))
                 hd[:] = d[:nc].cpu().numpy()
                 hp = O.aligned_empty((nc, m * S))
-                th = max(1, min(host_cores(), 16))
+                th = cpu_threads()
                 _, isa = O.encode_simd(k, m, S, hd, threads=th, out=hp)
-                ok = bool(np.array_equal(hp[:2], p[:2].cpu().numpy()))
+                ok = bool(np.array_equal(hp, p[:nc].cpu().numpy()))
                 cv, _, _ = _rate(lambda: O.encode_simd(k, m, S, hd, threads=th, isa=isa, out=hp),
                                  nc * B, 0.4)
+                hs = O.gather(k, m, S, hd, hp, s_idx[:nc])
+                ho = O.aligned_empty((nc, e * S))
+                O.rebuild_simd(k, m, S, s_idx[:nc], hs, l_idx[:nc], threads=th, isa=isa, out=ho)
+                ok = ok and bool(np.array_equal(ho, out[:nc].cpu().numpy()))
+                rv, _, _ = _rate(lambda: O.rebuild_simd(k, m, S, s_idx[:nc], hs, l_idx[:nc], threads=th,
+                                                        isa=isa, out=ho), nc * B, 0.4)
                 pt["cpu_GiBs"] = round(cv, 2)
+                pt["cpu_rebuild_GiBs"] = round(rv, 2)
                 pt["cpu_threads"] = th
                 pt["cpu_bit_exact"] = ok
             points.append(pt)
-            del d, p
-    segs, alg, pay = [], 0, 0
-    for (k, m) in [(4, 2), (10, 4), (16, 4)]:
+            del d, p, surv, want, out, sd, ld
+    segs, rsegs, checks, alg, ralg, pay = [], [], [], 0, 0, 0
+    for gi, (k, m) in enumerate([(4, 2), (10, 4), (16, 4)]):
         for B in [4 << 10, 64 << 10, 1 << 20, 4 << 20]:
             S = ec.shard_size(B, k)
             n = max(1, int(gib * 2**30 / 12) // B)
             d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
             p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
             codec.fill_blocks(SEED, 0, n, B, k, S, d)
+            codec.encode(k, m, d, p)
+            e, _, _, sd, ld, surv, want, out = rebuild_inputs(k, m, S, n, d, p, fb=gi)
             segs.append((k, m, S, n, d, p))
+            rsegs.append(dict(k=k, m=m, surv_idx=sd, surv=surv, lost_idx=ld, out=out))
+            checks.append((out, want))
             alg += (k + m) * S * n
+            ralg += (k + e) * S * n
             pay += n * B
-    _, (kms,), _ = timed_steps(torch, [lambda: codec.encode_segments(segs)], steps, warmup,
-                               settle_ms, None, stream)
-    ms = float(np.mean(kms))
+    _, (kms, rms), _ = timed_steps(torch, [lambda: codec.encode_segments(segs),
+                                           lambda: codec.rebuild_segments(rsegs)],
+                                   steps, warmup, settle_ms, None, stream)
+    codec.synchronize()
+    ms, rs = float(np.mean(kms)), float(np.mean(rms))
     fused = {"segments": len(segs), "kernel_ms": round(ms, 4),
-             "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
-             "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
-    return {"workload": "BASELINE.json C5: RS(k,m) encode per (k,m) x block size, ~%.1f GiB "
-                        "payload per point; fused = 12 mixed groups in one encode_segments call "
+             "GiBs": round(pay / (ms * 1e-3) / 2**30, 1), "frac": frac(alg, ms),
+             "rebuild": {"step_ms": round(rs, 4), "GiBs": round(pay / (rs * 1e-3) / 2**30, 1),
+                         "frac": frac(ralg, rs),
+                         "bit_exact": all(bool(torch.equal(o, w)) for o, w in checks)},
+             "encode_rebuild_GiBs": round(2 * pay / ((ms + rs) * 1e-3) / 2**30, 1)}
+    return {"workload": "BASELINE.json C5: RS(k,m) encode and rebuild (e = m random erasures per "
+                        "block) per (k,m) x block size, ~%.1f GiB payload per point; fused = 12 "
+                        "mixed groups in one encode_segments call and one rebuild_segments call "
                         "(one launch per code class)" % gib,
             "points": points, "fused": fused}
 
@@ -244,10 +295,46 @@ def _rate(fn, nbytes, seconds):
 
 
 def host_cores():
+    """CPUs in this process's affinity set (the whole machine on the GPU box)."""
     try:
         return len(os.sched_getaffinity(0))
     except AttributeError:
         return os.cpu_count() or 1
+
+
+def cpu_share():
+    """CPUs this process may actually keep busy: the affinity set, capped by
+    the cgroup CPU quota and by OMP_NUM_THREADS when set (the GPU box gives a
+    one-GPU job 16 CPUs of a 256-CPU machine; `nproc` reports 16 there)."""
+    n = host_cores()
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                per = int(f.read())
+            if q > 0:
+                n = min(n, max(1, q // per))
+        except (OSError, ValueError):
+            pass
+    try:
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
+        if omp > 0:
+            n = min(n, omp)
+    except ValueError:
+        pass
+    return n
+
+
+def cpu_threads():
+    """Threads of the CPU baseline: the CPU share, at most 16 (the GPU box's
+    share per GPU)."""
+    return max(1, min(cpu_share(), 16))
 
 
 def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
@@ -255,14 +342,13 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
     the same workload, and cross-check them against the GPU parity of the
     same blocks.  `value` is the vectorised encode (oracle/rs_simd.c:
     GFNI+AVX-512 affine or AVX2 split-nibble, ISA-L's published x86
-    techniques), the strongest CPU codec here, on 16 threads (the GPU box's
-    CPU share per GPU); every core the process may run on is timed beside it
-    (`all_cores`), and the scalar table oracle too.  Test infrastructure,
-    never the product."""
+    techniques), the strongest CPU codec here, on the process's CPU share
+    (cgroup quota / OMP_NUM_THREADS, at most 16: the GPU box's share per
+    GPU), one core beside it, and the scalar table oracle too.  Test
+    infrastructure, never the product."""
     from oracle import oracle as O
     O.build()
-    cores = host_cores()
-    threads = max(1, min(cores, 16))
+    threads = cpu_threads()
     nb = 128
     data = O.aligned_empty((nb, k * S))
     data[:] = O.fill_blocks(SEED, 0, nb, B, k, S)
@@ -275,16 +361,6 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                           nb * B, seconds)
     one, _, _ = _rate(lambda: O.encode_simd(k, m, S, data[:64], threads=1, isa=isa, out=par[:64]),
                       64 * B, 1.5)
-    # every affinity core, one block per thread per pass (at least 128 blocks)
-    nball = max(nb, cores)
-    if nball > nb:
-        dall = O.aligned_empty((nball, k * S))
-        dall[:] = np.resize(data, (nball, k * S))
-        pall = O.aligned_empty((nball, m * S))
-    else:
-        dall, pall = data, par
-    va, _, _ = _rate(lambda: O.encode_simd(k, m, S, dall, threads=cores, isa=isa, out=pall),
-                     nball * B, 3.0)
     sc_all, _, _ = _rate(lambda: O.encode(k, m, S, data[:32], threads=threads), 32 * B, 2.0)
     sc_one, _, _ = _rate(lambda: O.encode(k, m, S, data[:2], threads=1), 2 * B, 1.0)
     # the rebuild configs (C3): the same blocks, 4 random erasures each,
@@ -302,13 +378,13 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                                               isa=isa, out=rout[:16]), 16 * B, 1.0)
     return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": "RS(%d,%d) encode, %d x %d-byte blocks x %d passes (%.1f s), vectorised C port "
-                      "(%s, streaming stores) on %d threads; all %d affinity cores %.3f GiB/s; "
-                      "1-core %.3f GiB/s; scalar table oracle %.3f GiB/s on %d threads, %.3f on 1; "
-                      "bit-exact vs GPU on %d blocks: %s"
-                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, cores, va, one, sc_all,
+                      "(%s, streaming stores) on %d threads (the process's CPU share; %d CPUs in "
+                      "its affinity set); 1-core %.3f GiB/s; scalar table oracle %.3f GiB/s on %d "
+                      "threads, %.3f on 1; bit-exact vs GPU on %d blocks: %s"
+                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, host_cores(), one, sc_all,
                          threads, sc_one, nchk, ok_simd and ok_scalar),
             "isa": O.SIMD_ISA[isa], "single_core": round(one, 3),
-            "all_cores": {"cores": cores, "value": round(va, 3), "blocks": nball},
+            "cpu_share": cpu_share(), "affinity_cpus": host_cores(),
             "rebuild": {"value": round(rv, 3), "single_core": round(rone, 3), "threads": threads,
                         "erasures": e, "bit_exact": ok_reb,
                         "sample": "RS(%d,%d) rebuild of the same %d blocks, %d random erasures each "
@@ -326,7 +402,7 @@ def c1_case(torch, ec, codec, stream):
     from oracle import oracle as O
     k, m, B, n = 3, 2, 65536, 1000
     S = ec.shard_size(B, k)
-    threads = max(1, min(host_cores(), 16))
+    threads = cpu_threads()
     data = O.fill_blocks(SEED, 0, n, B, k, S)
     t0 = time.perf_counter()
     par = O.encode(k, m, S, data, threads=threads)
@@ -432,6 +508,125 @@ def sha_lines(torch, codec, stream, data, n, B):
             del msg
     return {"workload": "batched SHA-256(salt||owner||data) = CHB addresses (CHB.cc:264-289), "
                         "one lane per block", **res}
+
+
+def _visible_device(local):
+    """The device string a child process must see to use this rank's GPU."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v:
+            ids = [x for x in v.split(",") if x.strip()]
+            return var, ids[local] if local < len(ids) else ids[0]
+    return "HIP_VISIBLE_DEVICES", str(local)
+
+
+def pmc_traffic(args, result, local, world):
+    """roofline.traffic measured by this run: two rocprofv3 counter passes
+    (FETCH_SIZE, then WRITE_SIZE -- they cannot share a pass on gfx950) over
+    a short run of the same step on this rank's GPU, each a child process
+    started after the timed region.  HBM bytes per launch = 2 * FETCH_SIZE +
+    WRITE_SIZE (KiB units): on gfx950 FETCH_SIZE reports half the bytes of a
+    wide coalesced streaming read, WRITE_SIZE is exact for 16-byte-per-lane
+    stores (MI355X_MICROARCH.md, HBM).  The rebuild's traffic is its
+    kernels' per step (decode rows + MAC, or the fused kernel)."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+    k, m, B, n, e = args.k, args.m, args.block_bytes, args.blocks, args.erasures
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    env = {x: v for x, v in os.environ.items()
+           if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "MASTER_ADDR", "MASTER_PORT") and not x.startswith("TORCHELASTIC")}
+    if world > 1 and not args.same_device:
+        var, dev = _visible_device(local)
+        env[var] = dev
+    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "3", "--warmup", "1",
+             "--settle-ms", "0", "--no-small", "--no-cpu", "--no-e2e", "--no-pmc",
+             "--k", str(k), "--m", str(m), "--block-bytes", str(B), "--blocks", str(n),
+             "--erasures", str(e)]
+
+    def kind(name):
+        if "gf_mac_kernel" in name:
+            return "rebuild" if name.split("(")[0].rstrip(">").rstrip().endswith("true") else "encode"
+        if "gf_rebuild_kernel" in name or "decode_" in name:
+            return "rebuild_" + ("fused" if "gf_rebuild_kernel" in name else "decode")
+        return None
+
+    tmp = tempfile.mkdtemp(prefix="memo_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    per = {}
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            r = subprocess.run([rocprof, "--pmc", counter, "-d", d, "-o", "pmc", "-f", "csv", "--"] + child,
+                               env=env, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                               timeout=150)
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                raise RuntimeError("rocprofv3 --pmc %s: rc %d, %s" % (counter, r.returncode,
+                                                                      r.stderr.decode(errors="replace")[-300:]))
+            vals = {}
+            for f in files:
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        kd = kind(row.get("Kernel_Name", ""))
+                        if kd:
+                            vals.setdefault(kd, []).append(float(row["Counter_Value"]))
+            per[counter] = vals
+    except (OSError, RuntimeError, subprocess.SubprocessError, KeyError, ValueError) as ex:
+        for key in ("roofline", "roofline_rebuild"):
+            if key in result:
+                result[key]["traffic"] = None
+                result[key]["traffic_note"] = "counter passes failed: %s" % str(ex)[:300]
+        return
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+    def kb(counter, kd):
+        v = per.get(counter, {}).get(kd, [])
+        return float(np.median(v)) if v else 0.0
+
+    def traffic(kinds):
+        return int(round(sum(2 * kb("FETCH_SIZE", kd) + kb("WRITE_SIZE", kd) for kd in kinds) * 1024))
+
+    src = ("measured by this run: rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes (separate "
+           "child runs of the same step, 3 steps each, median launch), bytes = (2*FETCH_SIZE + "
+           "WRITE_SIZE) * 1024; build %s" % result["build_id"][:16])
+    enc = traffic(["encode"])
+    result["roofline"]["traffic"] = enc
+    result["roofline"]["traffic_ratio"] = round(enc / result["roofline"]["bytes_per_launch"], 4)
+    result["roofline"]["traffic_source"] = src
+    if "roofline_rebuild" in result:
+        kinds = [x for x in ("rebuild_decode", "rebuild", "rebuild_fused") if per["FETCH_SIZE"].get(x)]
+        rb = traffic(kinds)
+        result["roofline_rebuild"]["traffic"] = rb
+        result["roofline_rebuild"]["traffic_ratio"] = round(rb / result["roofline_rebuild"]["bytes_per_launch"], 4)
+        result["roofline_rebuild"]["traffic_kernels"] = kinds
+        result["roofline_rebuild"]["traffic_source"] = src
+
+
+def merge_extras(result, extras):
+    """Fold the ranks' side measurements (device copy rate, PCIe end-to-end
+    rates; one dict per rank, rank order) into the contract line (pure:
+    tested on CPU)."""
+    world = len(extras)
+    x0 = extras[0]
+    result["roofline"]["copy_GBs"] = round(x0["copy_GBs"], 1)
+    result["roofline"]["frac_of_copy"] = round(result["roofline"]["achieved"] / x0["copy_GBs"], 4)
+    if "e2e" not in x0:
+        return result
+    result["end_to_end"] = dict(x0["e2e"])
+    result["host_call_latency"] = x0["lat"]
+    if world > 1:
+        result["end_to_end"]["per_rank"] = [
+            {"rank": i, "pinned": x["e2e"]["pinned"]["value"], "pageable": x["e2e"]["pageable"]["value"]}
+            for i, x in enumerate(extras)]
+        result["end_to_end"]["node_sum"] = {
+            kind: round(sum(x["e2e"][kind]["value"] for x in extras), 3) for kind in ("pinned", "pageable")}
+        result["end_to_end"]["note"] = ("every rank streams over its own GPU's PCIe link at the same "
+                                        "time; node_sum adds the ranks' rates")
+    return result
 
 
 def assemble(args, world, rows, wall_max, S):
@@ -571,40 +766,47 @@ def main():
         wall_max = float(t.item())
     result = assemble(args, world, rows, wall_max, S)
 
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        try:
-            t = json.load(open(pmc))
-            for key, obj in (("encode_%d_%d_%d_%d" % (k, m, B, n), result["roofline"]),
-                             ("rebuild_%d_%d_%d_%d_e%d" % (k, m, B, n, e), result.get("roofline_rebuild"))):
-                if obj is not None and key in t:
-                    obj["traffic"] = t[key]["hbm_bytes_per_launch"]
-                    obj["traffic_source"] = t[key]["source"]
-        except (OSError, ValueError, KeyError):
-            pass
+    if args.no_pmc:
+        for key in ("roofline", "roofline_rebuild"):
+            if key in result:
+                result[key]["traffic_note"] = "not measured (--no-pmc)"
+    result["build_id"] = ec.build_id()
+    result["build_matches_sources"] = result["build_id"] == ec.source_id()
 
-    if world == 1:
-        # Measured HBM reference on this box: a device-to-
-        # device copy of the same data bytes on the same stream (read + write).
-        scratch = torch.empty_like(data)
-        _, (cms,), _ = timed_steps(torch, [lambda: scratch.copy_(data)], 10, 30, 0, None, stream)
-        copy_gbs = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
-        result["roofline"]["copy_GBs"] = round(copy_gbs, 1)
-        result["roofline"]["frac_of_copy"] = round(result["roofline"]["achieved"] / copy_gbs, 4)
-        del scratch
-        if not args.no_small:
-            result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps,
-                                                    args.warmup, args.settle_ms)
-        if not args.no_e2e:
-            result["end_to_end"], result["host_call_latency"] = end_to_end(
-                torch, ec, codec, data, par, k, m, B, n)
-            codec.set_stream(stream)
+    # ---- after the timed steps and their closing barrier: the baselines
+    # and side measurements, at every N.  Every rank measures its own GPU
+    # (device copy, PCIe end-to-end rate over its own link) concurrently;
+    # rank 0 alone times the CPU baseline and the counter passes while the
+    # others wait at the final barrier.
+    extra = {}
+    # Measured HBM reference on this box: a device-to-device
+    # copy of the same data bytes on the same stream (read + write).
+    scratch = torch.empty_like(data)
+    _, (cms,), _ = timed_steps(torch, [lambda: scratch.copy_(data)], 10, 30, 0, None, stream)
+    extra["copy_GBs"] = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
+    del scratch
+    if not args.no_e2e:
+        if dist is not None:
+            dist.barrier()  # all links busy at once, as on a node serving every GPU
+        extra["e2e"], extra["lat"] = end_to_end(torch, ec, codec, data, par, k, m, B, n)
+        codec.set_stream(stream)
+    extras = [extra]
+    if dist is not None:
+        extras = [None] * world
+        dist.all_gather_object(extras, extra)
+    merge_extras(result, extras)
+    if world == 1 and not args.no_small:
+        result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps,
+                                                args.warmup, args.settle_ms)
+    if rank == 0:
         if not args.no_cpu:
             result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, par[:4].cpu().numpy())
             result["c1"] = c1_case(torch, ec, codec, stream)
+        if not args.no_pmc:
+            pmc_traffic(args, result, local, world)
         if args.sha:
             result["sha256"] = sha_lines(torch, codec, stream, data, n, B)
-        if args.sweep:
+        if args.sweep and world == 1:
             del data, par
             result["sweep"] = sweep(torch, ec, codec, stream, args.sweep_gib, max(3, args.steps // 4),
                                     args.warmup, args.settle_ms, cpu=not args.no_cpu)

@@ -184,6 +184,53 @@ void Codec::rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* sur
   ++uniform_calls_;
 }
 
+void Codec::rebuild_segments(const std::vector<memo_ec_rebuild_segment>& segs, bool pinned) {
+  const int where = pinned ? MEMO_EC_HOST_PINNED : MEMO_EC_HOST;
+  size_t maxn = 0;
+  for (const auto& sg : segs) maxn = std::max(maxn, sg.n);
+  // device d rebuilds blocks [d * per, (d + 1) * per) of every segment
+  const size_t D = (dev_.size() > 1 && maxn >= 2 * dev_.size()) ? dev_.size() : 1;
+  auto part = [&](size_t d) {
+    std::vector<memo_ec_rebuild_segment> mine;
+    for (const auto& sg : segs) {
+      const size_t per = (sg.n + D - 1) / D, b0 = std::min(sg.n, d * per), cnt = std::min(per, sg.n - b0);
+      if (cnt == 0) continue;
+      memo_ec_rebuild_segment x = sg;
+      x.n = cnt;
+      x.surv = sg.surv + b0 * sg.k * sg.S;
+      x.out = sg.out + b0 * (size_t)sg.e * sg.S;
+      if (!sg.uniform) {
+        x.surv_idx = sg.surv_idx + b0 * sg.k;
+        x.lost_idx = sg.lost_idx + b0 * (size_t)sg.e;
+      }
+      mine.push_back(x);
+    }
+    return mine;
+  };
+  auto run = [&](size_t dslot, const std::vector<memo_ec_rebuild_segment>& mine) {
+    auto* c = acquire(dslot);
+    int rc = MEMO_EC_OK;
+    for (size_t i = 0; i < mine.size() && rc == MEMO_EC_OK; i += MEMO_EC_MAX_REBUILD_SEGMENTS) {
+      const int cnt = (int)std::min<size_t>(MEMO_EC_MAX_REBUILD_SEGMENTS, mine.size() - i);
+      rc = memo_ec_rebuild_segments(c, cnt, mine.data() + i, where);
+    }
+    release(dslot, c);
+    return rc;
+  };
+  if (D == 1) {
+    const size_t d = dev_.size() == 1 ? 0 : rr_++ % dev_.size();
+    check(run(d, part(0)), "rebuild_segments");
+  } else {
+    std::vector<int> rc(D, MEMO_EC_OK);
+    std::vector<std::thread> ts;
+    for (size_t d = 0; d < D; ++d) ts.emplace_back([&, d] { rc[d] = run(d, part(d)); });
+    for (auto& t : ts) t.join();
+    for (int r : rc) check(r, "rebuild_segments");
+  }
+  ++segments_calls_;
+  for (const auto& sg : segs) uniform_segments_ += sg.uniform ? 1 : 0;
+}
+
 // ------------------------------------------------------- pinned arena
 PinnedArena::Lease& PinnedArena::Lease::operator=(Lease&& o) noexcept {
   if (this != &o) {
@@ -444,8 +491,10 @@ ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& 
       pool_(o.threads) {
   if (o_.k < 1 || o_.m < 1 || o_.k > MEMO_EC_MAX_K || o_.m > MEMO_EC_MAX_M)
     throw Error("erasure: bad (k, m)");
-  bthread_ = std::thread([this] { batcher_loop(); });
+  // the index first: rescan() may throw (silo listing), and must do so before
+  // any thread of this object exists
   if (o_.rescan) rescan();
+  bthread_ = std::thread([this] { batcher_loop(); });
   mthread_ = std::thread([this] { membership_loop(); });
   Overlay::Handlers h;
   h.discovered = [this](const Address& id) { post(kDiscovered, id); };
@@ -482,13 +531,31 @@ std::string ErasureConsensus::redundancy() const {
                   {"desired_factor", f}});
 }
 
+size_t ErasureConsensus::under_placed() const {
+  std::shared_lock<std::shared_mutex> g(index_mu_);
+  size_t n = 0;
+  for (auto& kv : index_)
+    n += std::any_of(kv.second.holder.begin(), kv.second.holder.end(), [](const Address& h) { return !h; });
+  return n;
+}
+
 std::string ErasureConsensus::stats() const {
-  size_t blocks;
+  size_t blocks, under = 0;
+  std::string sample;
   {
     std::shared_lock<std::shared_mutex> g(index_mu_);
     blocks = index_.size();
+    size_t ns = 0;
+    for (auto& kv : index_)
+      if (std::any_of(kv.second.holder.begin(), kv.second.holder.end(), [](const Address& h) { return !h; })) {
+        ++under;
+        if (ns++ < 10) sample += (sample.empty() ? "" : " ") + kv.first.hex();
+      }
   }
   return to_json({{"blocks", std::to_string(blocks)},
+                  {"under_placed", std::to_string(under)},
+                  {"sample_under_placed", sample},
+                  {"segments_calls", std::to_string(codec_.segments_calls())},
                   {"stored", std::to_string(stored_)},
                   {"fetched", std::to_string(fetched_)},
                   {"decoded", std::to_string(decoded_)},
@@ -629,6 +696,18 @@ size_t NodeIndex::count(const Address& node) const {
 void ErasureConsensus::on_rebalanced(std::function<void(const Address&)> f) {
   std::lock_guard<std::mutex> g(repair_mu_);
   rebalanced_ = std::move(f);
+}
+
+void ErasureConsensus::on_under_placed(std::function<void(const Address&, int)> f) {
+  std::lock_guard<std::mutex> g(repair_mu_);
+  under_placed_ = std::move(f);
+}
+
+void ErasureConsensus::notify_under_placed(const std::vector<std::pair<Address, int>>& v) {
+  if (v.empty()) return;
+  std::lock_guard<std::mutex> g(repair_mu_);
+  if (under_placed_)
+    for (auto& x : v) under_placed_(x.first, x.second);
 }
 
 // The batcher thread: gathers concurrent store() calls (up to batch_max
@@ -1022,9 +1101,12 @@ std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
 }
 
 // Multi-address fetch: shards of all blocks gathered on the pool, then ONE
-// GPU rebuild per (shard-size bucket, erasure count) group of the blocks
-// that miss data shards (zero-padded to the group's largest shard), then
-// reassembly + CHB check on the pool; `res` is called in request order.
+// codec call (memo_ec_rebuild_segments) for every block that misses data
+// shards -- a segment per (shard-size bucket, erasure count) group, shards
+// zero-padded to the group's largest, and per shared erasure pattern --
+// then reassembly + CHB check on the pool; `res` is called in request
+// order.  The reference hands the whole batch over at once too
+// (Consensus::_fetch(vector<AddressVersion>), Consensus.cc:101-124).
 void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
   const int k = o_.k, m = o_.m;
   const size_t n = addresses.size();
@@ -1089,39 +1171,80 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   };
   pool_.parallel_for(direct.size(), [&](size_t t) { finish(direct[t], nullptr, 0); });
   tm.lap("assemble_direct");
-  for (auto& grp : groups) {
-    const int e = grp.e;
-    auto& ids = grp.ids;
-    for (size_t b0 = 0; b0 < ids.size(); b0 += o_.batch_max) {
-      const size_t nb = std::min<size_t>(o_.batch_max, ids.size() - b0);
-      size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
-      for (size_t bi = 0; bi < nb; ++bi) S = std::max(S, (size_t)g[ids[b0 + bi]].h.shard_size);
-      std::vector<uint8_t> sidx(nb * k), lidx(nb * e);
-      auto surv = arena_.lease(nb * k * S), out = arena_.lease(nb * e * S);
-      const bool pin = surv.pinned() && out.pinned();
-      tm.lap("alloc");
-      pool_.parallel_for(nb, [&](size_t bi) {
-        Gathered& x = g[ids[b0 + bi]];
-        for (int s = 0; s < k; ++s) {
-          sidx[bi * k + s] = (uint8_t)x.shards[s].first;
-          uint8_t* slot = surv.data() + (bi * k + s) * S;
-          std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
-          std::memset(slot + x.h.shard_size, 0, S - x.h.shard_size);
-        }
-        std::copy(x.lost.begin(), x.lost.end(), lidx.begin() + bi * e);
-      });
-      tm.lap("copy_in");
-      if (grp.uniform)
-        codec_.rebuild_uniform(k, m, S, nb, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
-                               out.data(), pin);
-      else
-        codec_.rebuild(k, m, S, nb, sidx.data(), surv.data(), lidx.data(), e, out.data(), pin);
-      tm.lap("rebuild");
-      decoded_ += nb;
-      pool_.parallel_for(nb, [&](size_t bi) { finish(ids[b0 + bi], out.data() + bi * e * S, S); });
-      tm.lap("assemble");
+  // every group's batches staged, then ONE codec call for all of them
+  // (memo_ec_rebuild_segments: a segment per batch), then reassembly
+  struct FBatch {
+    const FGroup* grp;
+    size_t b0, nb, S;
+    std::vector<uint8_t> sidx, lidx;
+    PinnedArena::Lease surv, out;
+  };
+  std::vector<FBatch> batches;
+  for (auto& grp : groups)
+    for (size_t b0 = 0; b0 < grp.ids.size(); b0 += o_.batch_max) {
+      FBatch fb;
+      fb.grp = &grp;
+      fb.b0 = b0;
+      fb.nb = std::min<size_t>(o_.batch_max, grp.ids.size() - b0);
+      fb.S = 0;  // the batch's largest shard; smaller shards zero-padded
+      for (size_t bi = 0; bi < fb.nb; ++bi) fb.S = std::max(fb.S, (size_t)g[grp.ids[b0 + bi]].h.shard_size);
+      batches.push_back(std::move(fb));
+    }
+  bool pin = true;
+  for (auto& fb : batches) {
+    const int e = fb.grp->e;
+    fb.surv = arena_.lease(fb.nb * k * fb.S);
+    fb.out = arena_.lease(fb.nb * e * fb.S);
+    pin = pin && fb.surv.pinned() && fb.out.pinned();
+    if (!fb.grp->uniform) {
+      fb.sidx.resize(fb.nb * k);
+      fb.lidx.resize(fb.nb * e);
     }
   }
+  tm.lap("alloc");
+  // (batch, block) pairs copied in on the pool
+  std::vector<std::pair<size_t, size_t>> work;
+  for (size_t x = 0; x < batches.size(); ++x)
+    for (size_t bi = 0; bi < batches[x].nb; ++bi) work.emplace_back(x, bi);
+  pool_.parallel_for(work.size(), [&](size_t t) {
+    FBatch& fb = batches[work[t].first];
+    const size_t bi = work[t].second;
+    Gathered& x = g[fb.grp->ids[fb.b0 + bi]];
+    for (int s = 0; s < k; ++s) {
+      uint8_t* slot = fb.surv.data() + (bi * k + s) * fb.S;
+      std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
+      std::memset(slot + x.h.shard_size, 0, fb.S - x.h.shard_size);
+      if (!fb.grp->uniform) fb.sidx[bi * k + s] = (uint8_t)x.shards[s].first;
+    }
+    if (!fb.grp->uniform) std::copy(x.lost.begin(), x.lost.end(), fb.lidx.begin() + bi * fb.grp->e);
+  });
+  tm.lap("copy_in");
+  if (!batches.empty()) {
+    std::vector<memo_ec_rebuild_segment> segs;
+    for (auto& fb : batches) {
+      memo_ec_rebuild_segment sg{};
+      sg.k = k;
+      sg.m = m;
+      sg.S = fb.S;
+      sg.n = fb.nb;
+      sg.e = fb.grp->e;
+      sg.uniform = fb.grp->uniform ? 1 : 0;
+      sg.surv = fb.surv.data();
+      sg.out = fb.out.data();
+      sg.surv_idx = fb.grp->uniform ? fb.grp->pat.data() : fb.sidx.data();
+      sg.lost_idx = fb.grp->uniform ? fb.grp->pat.data() + k : fb.lidx.data();
+      segs.push_back(sg);
+    }
+    codec_.rebuild_segments(segs, pin);
+    tm.lap("rebuild");
+  }
+  for (auto& fb : batches) decoded_ += fb.nb;
+  pool_.parallel_for(work.size(), [&](size_t t) {
+    FBatch& fb = batches[work[t].first];
+    const size_t bi = work[t].second;
+    finish(fb.grp->ids[fb.b0 + bi], fb.out.data() + bi * fb.grp->e * fb.S, fb.S);
+  });
+  tm.lap("assemble");
   for (size_t i = 0; i < n; ++i) res(addresses[i], std::move(blocks[i]), errs[i]);
 }
 
@@ -1241,9 +1364,6 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       }
       work.push_back(&x);
     }
-    // Batches of blocks with the same (S bucket, e): one GPU rebuild call
-    // each; blocks that also share their erasure pattern -- the repair of
-    // one lost node -- take the uniform rebuild (shared tables, encode speed).
     struct Group {
       int e;
       bool uniform;
@@ -1268,117 +1388,167 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         for (auto* x : bp.second) rest[{bp.first.first, (size_t)e}].push_back(x);
     }
     for (auto& r : rest) gs.push_back({(int)r.first.second, false, {}, r.second});
-    for (auto& grp : gs) {
-      const int e = grp.e;
+    // Batches of blocks with the same (S bucket, e), or the same erasure
+    // pattern (the repair of one lost node: shared tables, encode speed),
+    // all rebuilt by ONE codec call per chunk (memo_ec_rebuild_segments, a
+    // segment per batch), then placed batch by batch.
+    struct RBatch {
+      const Group* grp;
+      size_t b0, n, S;
+      std::vector<uint8_t> sidx, lidx;
+      PinnedArena::Lease surv, out;
+    };
+    std::vector<RBatch> rbs;
+    bool pin = true;
+    for (auto& grp : gs)
       for (size_t b0 = 0; b0 < grp.items.size(); b0 += o_.batch_max) {
-        const size_t n = std::min<size_t>(o_.batch_max, grp.items.size() - b0);
-        size_t S = 0;  // the batch's largest shard; smaller shards zero-padded
-        for (size_t bi = 0; bi < n; ++bi) S = std::max(S, memo_ec_shard_size(grp.items[b0 + bi]->pl.B, k));
-        std::vector<uint8_t> sidx(n * k), lidx(n * e);
-        auto surv = arena_.lease(n * k * S), out = arena_.lease(n * e * S);
-        const bool pin = surv.pinned() && out.pinned();
-        pool_.parallel_for(n, [&](size_t bi) {
-          Todo& x = *grp.items[b0 + bi];
-          const size_t Sb = memo_ec_shard_size(x.pl.B, k);
-          for (int s = 0; s < k; ++s) {
-            uint8_t* slot = surv.data() + (bi * k + s) * S;
-            std::memcpy(slot, x.surv[s].second.data() + ShardHeader::kSize, Sb);
-            std::memset(slot + Sb, 0, S - Sb);
-            sidx[bi * k + s] = (uint8_t)x.surv[s].first;
+        RBatch rb;
+        rb.grp = &grp;
+        rb.b0 = b0;
+        rb.n = std::min<size_t>(o_.batch_max, grp.items.size() - b0);
+        rb.S = 0;  // the batch's largest shard; smaller shards zero-padded
+        for (size_t bi = 0; bi < rb.n; ++bi) rb.S = std::max(rb.S, memo_ec_shard_size(grp.items[b0 + bi]->pl.B, k));
+        rb.surv = arena_.lease(rb.n * k * rb.S);
+        rb.out = arena_.lease(rb.n * grp.e * rb.S);
+        pin = pin && rb.surv.pinned() && rb.out.pinned();
+        rb.sidx.resize(rb.n * k);
+        rb.lidx.resize(rb.n * grp.e);
+        rbs.push_back(std::move(rb));
+      }
+    std::vector<std::pair<size_t, size_t>> units;  // (batch, block)
+    for (size_t x = 0; x < rbs.size(); ++x)
+      for (size_t bi = 0; bi < rbs[x].n; ++bi) units.emplace_back(x, bi);
+    pool_.parallel_for(units.size(), [&](size_t t) {
+      RBatch& rb = rbs[units[t].first];
+      const size_t bi = units[t].second, S = rb.S;
+      const int e = rb.grp->e;
+      Todo& x = *rb.grp->items[rb.b0 + bi];
+      const size_t Sb = memo_ec_shard_size(x.pl.B, k);
+      for (int s = 0; s < k; ++s) {
+        uint8_t* slot = rb.surv.data() + (bi * k + s) * S;
+        std::memcpy(slot, x.surv[s].second.data() + ShardHeader::kSize, Sb);
+        std::memset(slot + Sb, 0, S - Sb);
+        rb.sidx[bi * k + s] = (uint8_t)x.surv[s].first;
+      }
+      for (int r = 0; r < e; ++r) rb.lidx[bi * e + r] = (uint8_t)x.lost[r];
+      x.surv.clear();
+      x.surv.shrink_to_fit();
+    });
+    tm.lap("copy_in");
+    if (!rbs.empty()) {
+      std::vector<memo_ec_rebuild_segment> segs;
+      for (auto& rb : rbs) {
+        memo_ec_rebuild_segment sg{};
+        sg.k = k;
+        sg.m = m;
+        sg.S = rb.S;
+        sg.n = rb.n;
+        sg.e = rb.grp->e;
+        sg.uniform = rb.grp->uniform ? 1 : 0;
+        sg.surv = rb.surv.data();
+        sg.out = rb.out.data();
+        sg.surv_idx = rb.grp->uniform ? rb.grp->pat.data() : rb.sidx.data();
+        sg.lost_idx = rb.grp->uniform ? rb.grp->pat.data() + k : rb.lidx.data();
+        segs.push_back(sg);
+      }
+      codec_.rebuild_segments(segs, pin);
+      ++rep.codec_calls;
+      tm.lap("rebuild");
+    }
+    for (auto& rb : rbs) {
+      const size_t n = rb.n, S = rb.S;
+      const int e = rb.grp->e;
+      std::vector<int> placed(n, 0);
+      // place each rebuilt shard on a reachable node holding none of the
+      // block's other shards (Overlay::allocate order); the stale copy on
+      // a reachable old holder is dropped
+      pool_.parallel_for(n, [&](size_t bi) {
+        Todo& x = *rb.grp->items[rb.b0 + bi];
+        std::set<Address> taken;
+        for (int i = 0; i < total; ++i)
+          if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
+            taken.insert(x.pl.holder[i]);
+        auto cand = overlay_.allocate(x.a, (int)overlay_.size());
+        const ShardKeys keys(x.a);
+        size_t ci = 0;
+        for (int r = 0; r < e; ++r) {
+          const int i = x.lost[r];
+          const Address old = x.pl.holder[i];
+          const Buffer wire = encode_shard(header_of(x.a, x.pl, i), rb.out.data() + (bi * e + r) * S);
+          x.pl.holder[i] = Address();
+          while (ci < cand.size()) {
+            auto& nd = cand[ci++];
+            if (taken.count(nd->id)) continue;
+            try {
+              nd->store(keys(i), wire);
+              x.pl.holder[i] = nd->id;
+              taken.insert(nd->id);
+              ++placed[bi];
+              break;
+            } catch (Unavailable&) {
+            }
           }
-          for (int r = 0; r < e; ++r) lidx[bi * e + r] = (uint8_t)x.lost[r];
-          x.surv.clear();
-          x.surv.shrink_to_fit();
-        });
-        tm.lap("copy_in");
-        if (grp.uniform)
-          codec_.rebuild_uniform(k, m, S, n, grp.pat.data(), surv.data(), grp.pat.data() + k, e,
-                                 out.data(), pin);
-        else
-          codec_.rebuild(k, m, S, n, sidx.data(), surv.data(), lidx.data(), e, out.data(), pin);
-        ++rep.codec_calls;
-        tm.lap("rebuild");
-        std::vector<int> placed(n, 0);
-        // place each rebuilt shard on a reachable node holding none of the
-        // block's other shards (Overlay::allocate order); the stale copy on
-        // a reachable old holder is dropped
-        pool_.parallel_for(n, [&](size_t bi) {
-          Todo& x = *grp.items[b0 + bi];
-          std::set<Address> taken;
-          for (int i = 0; i < total; ++i)
-            if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
-              taken.insert(x.pl.holder[i]);
-          auto cand = overlay_.allocate(x.a, (int)overlay_.size());
-          const ShardKeys keys(x.a);
-          size_t ci = 0;
-          for (int r = 0; r < e; ++r) {
-            const int i = x.lost[r];
-            const Address old = x.pl.holder[i];
-            const Buffer wire = encode_shard(header_of(x.a, x.pl, i), out.data() + (bi * e + r) * S);
-            x.pl.holder[i] = Address();
-            while (ci < cand.size()) {
-              auto& nd = cand[ci++];
-              if (taken.count(nd->id)) continue;
+          if (old && old != x.pl.holder[i]) {
+            auto on = overlay_.node(old);
+            if (on && on->up && !on->evicted) {
               try {
-                nd->store(keys(i), wire);
-                x.pl.holder[i] = nd->id;
-                taken.insert(nd->id);
-                ++placed[bi];
-                break;
-              } catch (Unavailable&) {
+                on->remove(keys(i));
+              } catch (Error&) {
               }
             }
-            if (old && old != x.pl.holder[i]) {
-              auto on = overlay_.node(old);
-              if (on && on->up && !on->evicted) {
+          }
+        }
+      });
+      tm.lap("place");
+      // the batch's new placements enter the index under one lock
+      std::vector<char> gone(n, 0);
+      std::vector<NodeIndex::Change> ch;
+      ch.reserve(n);
+      {
+        std::unique_lock<std::shared_mutex> lk(index_mu_);
+        for (size_t bi = 0; bi < n; ++bi) {
+          Todo& x = *rb.grp->items[rb.b0 + bi];
+          if (!index_.count(x.a)) {
+            gone[bi] = 1;
+            continue;
+          }
+          NodeIndex::Change c;
+          c.block = x.a;
+          c.new_h = x.pl.holder;
+          c.old_h = swap_placement_locked(x.a, std::move(x.pl));  // x.pl unused from here
+          ch.push_back(std::move(c));
+        }
+      }
+      nodes_.update_many(ch);
+      tm.lap("index");
+      for (size_t bi = 0; bi < n; ++bi) {
+        Todo& x = *rb.grp->items[rb.b0 + bi];
+        if (gone[bi]) {  // removed while being repaired: drop the new shards
+          for (int i : x.lost)
+            if (x.pl.holder[i])
+              if (auto nd = overlay_.node(x.pl.holder[i])) {
                 try {
-                  on->remove(keys(i));
+                  nd->remove(shard_key(x.a, i));
                 } catch (Error&) {
                 }
               }
-            }
-          }
-        });
-        tm.lap("place");
-        // the batch's new placements enter the index under one lock
-        std::vector<char> gone(n, 0);
-        std::vector<NodeIndex::Change> ch;
-        ch.reserve(n);
-        {
-          std::unique_lock<std::shared_mutex> lk(index_mu_);
-          for (size_t bi = 0; bi < n; ++bi) {
-            Todo& x = *grp.items[b0 + bi];
-            if (!index_.count(x.a)) {
-              gone[bi] = 1;
-              continue;
-            }
-            NodeIndex::Change c;
-            c.block = x.a;
-            c.new_h = x.pl.holder;
-            c.old_h = swap_placement_locked(x.a, std::move(x.pl));  // x.pl unused from here
-            ch.push_back(std::move(c));
-          }
+          continue;
         }
-        nodes_.update_many(ch);
-        tm.lap("index");
-        for (size_t bi = 0; bi < n; ++bi) {
-          Todo& x = *grp.items[b0 + bi];
-          if (gone[bi]) {  // removed while being repaired: drop the new shards
-            for (int i : x.lost)
-              if (x.pl.holder[i])
-                if (auto nd = overlay_.node(x.pl.holder[i])) {
-                  try {
-                    nd->remove(shard_key(x.a, i));
-                  } catch (Error&) {
-                  }
-                }
-            continue;
+        ++rep.blocks_repaired;
+        rep.shards_rebuilt += (size_t)placed[bi];
+        rep.shards_unplaced += (size_t)e - (size_t)placed[bi];
+        ++repaired_;
+        if (rebalanced_ && placed[bi]) rebalanced_(x.a);  // moved onto new owners
+        if (placed[bi] < e && under_placed_) {
+          // no reachable node could take the rest (Paxos.cc:1120-1126)
+          int held = 0;
+          {
+            std::shared_lock<std::shared_mutex> lk(index_mu_);
+            auto it = index_.find(x.a);
+            if (it != index_.end())
+              for (auto& h : it->second.holder) held += h ? 1 : 0;
           }
-          ++rep.blocks_repaired;
-          rep.shards_rebuilt += (size_t)placed[bi];
-          rep.shards_unplaced += (size_t)e - (size_t)placed[bi];
-          ++repaired_;
-          if (rebalanced_ && placed[bi]) rebalanced_(x.a);  // moved onto new owners
+          under_placed_(x.a, held);
         }
       }
     }
@@ -1518,7 +1688,11 @@ void ErasureConsensus::membership_loop() {
         if (o_.eviction_delay_ms >= 0)
           evict_at_[ev.second] = clock::now() + std::chrono::milliseconds(o_.eviction_delay_ms);
       } else if (ev.first == kAppeared) {
+        // a returning node is a discovery too (Paxos::_discovered clears the
+        // timeout and queues rebalancing, Paxos.cc:969-975): blocks stored
+        // while it was away can take their missing shards now
         evict_at_.erase(ev.second);
+        expand_now = expand_now || o_.auto_expand;
       } else if (ev.first == kUnderPlaced) {
         if (under_.empty()) under_at_ = clock::now();
         under_.insert(ev.second);
@@ -1553,29 +1727,40 @@ void ErasureConsensus::membership_loop() {
       // discovery (Paxos: _under_replicated when no new owner exists,
       // Paxos.cc:1120-1124), so a network smaller than k+m does not decode
       // every store's missing shards for nothing.
-      auto placeable = [&](const std::vector<Address>& v) {
-        size_t reachable = 0;
-        for (auto& n : overlay_.nodes()) reachable += (n->up && !n->evicted) ? 1 : 0;
+      // A block is placeable while some reachable node holds none of its
+      // shards (holders that are down still count as holders: they keep
+      // their shards); the others are reported under-placed.
+      auto placeable = [&](const std::vector<Address>& v, std::vector<std::pair<Address, int>>* stuck) {
+        std::vector<Address> reach;
+        for (auto& n : overlay_.nodes())
+          if (n->up && !n->evicted) reach.push_back(n->id);
         std::vector<Address> out;
         std::shared_lock<std::shared_mutex> g(index_mu_);
         for (auto& a : v) {
           auto it = index_.find(a);
           if (it == index_.end()) continue;  // removed
-          const size_t held = (size_t)std::count_if(it->second.holder.begin(), it->second.holder.end(),
-                                                    [](const Address& h) { return (bool)h; });
-          if (held < it->second.holder.size() && reachable > held) out.push_back(a);
+          const auto& hv = it->second.holder;
+          const int held = (int)std::count_if(hv.begin(), hv.end(), [](const Address& h) { return (bool)h; });
+          if (held == (int)hv.size()) continue;  // placed meanwhile
+          const bool free = std::any_of(reach.begin(), reach.end(), [&](const Address& r) {
+            return std::find(hv.begin(), hv.end(), r) == hv.end();
+          });
+          if (free) out.push_back(a);
+          else if (stuck) stuck->emplace_back(a, held);
         }
         return out;
       };
-      const std::vector<Address> todo = placeable(retry);
+      std::vector<std::pair<Address, int>> stuck;
+      const std::vector<Address> todo = placeable(retry, &stuck);
       if (!todo.empty()) {
         try {
           repair_blocks(todo, false);
         } catch (std::exception& e) {
           std::fprintf(stderr, "erasure: rebalancing failed: %s\n", e.what());
         }
-        again = placeable(todo);  // e.g. the candidate refused: try again later
+        again = placeable(todo, nullptr);  // e.g. the candidate refused: try again later
       }
+      notify_under_placed(stuck);
     }
     for (auto& id : due) {
       auto nd = overlay_.node(id);

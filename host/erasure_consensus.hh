@@ -59,9 +59,16 @@ class Codec {
   void rebuild_uniform(int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                        const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
                        bool pinned = false);
+  // Groups with different shard sizes, erasure counts and per-block or
+  // shared patterns in one library call per device
+  // (memo_ec_rebuild_segments); every device takes its share of every group.
+  void rebuild_segments(const std::vector<memo_ec_rebuild_segment>& segs, bool pinned = false);
   uint64_t encode_calls() const { return encode_calls_; }
   uint64_t rebuild_calls() const { return rebuild_calls_; }
   uint64_t uniform_calls() const { return uniform_calls_; }
+  uint64_t segments_calls() const { return segments_calls_; }
+  // segments with one shared erasure pattern passed to rebuild_segments
+  uint64_t uniform_segments() const { return uniform_segments_; }
   size_t devices() const { return dev_.size(); }
 
  private:
@@ -79,7 +86,8 @@ class Codec {
   std::vector<memo_ec_ctx*> all_;
   std::vector<Dev> dev_;
   std::atomic<size_t> rr_{0};
-  std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0}, uniform_calls_{0};
+  std::atomic<uint64_t> encode_calls_{0}, rebuild_calls_{0}, uniform_calls_{0}, segments_calls_{0},
+      uniform_segments_{0};
 };
 
 // ------------------------------------------------------- pinned arena
@@ -278,6 +286,16 @@ class ErasureConsensus : public StackedConsensus {
   // Called after a block's shards were rebuilt or re-placed (the reference's
   // rebalanced() signal); runs on the repairing thread.
   void on_rebalanced(std::function<void(const Address&)> f);
+  // Called with (block, holders) when a block is left on fewer than k+m
+  // owners because no reachable node can take its missing shards (after a
+  // repair, or when a background retry finds no free node): the reference's
+  // under_replicated(address, quorum size) signal (Paxos.hh:366-370, fired
+  // at Paxos.cc:1126).  Runs on the repairing / membership thread.
+  void on_under_placed(std::function<void(const Address&, int)> f);
+  // Blocks currently on fewer than k+m owners (the
+  // underreplicated_immutable_blocks gauge, src/memo/overlay/Overlay.cc:35-40);
+  // stats() reports it with a sample of up to 10 addresses.
+  size_t under_placed() const;
   // Blocks the per-node index lists for `node` (Paxos.hh:403-434 by_node).
   size_t node_blocks(const Address& node) const;
   // Evictions scheduled and not yet run.
@@ -362,6 +380,8 @@ class ErasureConsensus : public StackedConsensus {
   NodeIndex nodes_;  // node -> blocks it holds a shard of
   std::mutex repair_mu_;  // one repair engine run at a time
   std::function<void(const Address&)> rebalanced_;
+  std::function<void(const Address&, int)> under_placed_;  // guarded by repair_mu_
+  void notify_under_placed(const std::vector<std::pair<Address, int>>& v);
   // batcher (host C++ batching of concurrent stores into one GPU call)
   std::mutex bmu_;
   std::condition_variable bcv_;

@@ -52,12 +52,13 @@
 extern "C" {
 #endif
 
-#define MEMO_EC_VERSION 1
+#define MEMO_EC_VERSION 2
 
 /* Limits of this implementation. */
 #define MEMO_EC_MAX_K 64
 #define MEMO_EC_MAX_M 16
-#define MEMO_EC_MAX_SEGMENTS 12
+#define MEMO_EC_MAX_SEGMENTS 12          /* memo_ec_encode_segments  */
+#define MEMO_EC_MAX_REBUILD_SEGMENTS 256 /* memo_ec_rebuild_segments */
 
 typedef struct memo_ec_ctx memo_ec_ctx;
 
@@ -89,6 +90,50 @@ typedef struct memo_ec_segment {
     uint8_t *parity;     /* device: n x m x S */
 } memo_ec_segment;
 
+/* One (k, m, S) group of blocks of a mixed-geometry rebuild
+ * (memo_ec_rebuild_segments).  Per-block patterns (uniform == 0): surv_idx
+ * n x k and lost_idx n x e, in the memory `where` names.  One pattern for
+ * the group (uniform != 0, the repair of one lost node): surv_idx k and
+ * lost_idx e bytes in host memory, as for memo_ec_rebuild_uniform. */
+typedef struct memo_ec_rebuild_segment {
+    int k, m;
+    size_t S, n;
+    const uint8_t *surv_idx;
+    const uint8_t *surv;     /* n x k x S, in surv_idx order     */
+    const uint8_t *lost_idx;
+    int e;                   /* lost shards per block, 0..m     */
+    int uniform;
+    uint8_t *out;            /* n x e x S, in lost_idx order     */
+} memo_ec_rebuild_segment;
+
+/* Per-context tuning (memo_ec_ctx_set_option).  Each starts from the
+ * environment variable named beside it, read once by memo_ec_ctx_create. */
+enum memo_ec_option {
+    MEMO_EC_OPT_REBUILD_PATH = 1,       /* MEMO_EC_REBUILD_FUSED: -1 auto (default),
+                                           0 decode rows + MAC, 1 fused kernel   */
+    MEMO_EC_OPT_FUSED_MAX_BYTES = 2,    /* MEMO_EC_FUSED_MAX_MB: auto takes the fused
+                                           kernel up to this many survivor bytes
+                                           per call (64 MiB)                     */
+    MEMO_EC_OPT_ZERO_COPY_BYTES = 3,    /* MEMO_EC_ZC_KB: host calls moving at most
+                                           this many bytes run their kernels on
+                                           pinned host memory (4 MiB; 0: off)    */
+    MEMO_EC_OPT_PIPE_BYTES = 4,         /* MEMO_EC_PIPE_MB: host pipeline batch
+                                           (64 MiB)                              */
+    MEMO_EC_OPT_COPY_THREADS = 5,       /* MEMO_EC_COPY_THREADS: threads per pageable
+                                           bounce copy (0: the shared pool's all) */
+    MEMO_EC_OPT_MAX_LAUNCH_TILES = 6,   /* MEMO_EC_MAX_LAUNCH_TILES: tiles per MAC
+                                           launch (0: the 31-bit grid limit)     */
+    MEMO_EC_OPT_XCD_MIN_TILES = 7,      /* MEMO_EC_XCD_MIN_TILES: smallest segment
+                                           given the XCD-contiguous tile order   */
+    MEMO_EC_OPT_DECODE_WIDE_MAX = 8,    /* MEMO_EC_DECODE_WIDE_MAX: decode-row batches
+                                           up to this many blocks take the
+                                           column-per-lane kernel (65536)        */
+    MEMO_EC_OPT_DECODE_EXACT = 9,       /* MEMO_EC_DECODE_EXACT: exact-k decode
+                                           kernels (1)                           */
+    MEMO_EC_OPT_DECODE_STAGE = 10       /* MEMO_EC_DECODE_STAGE: decode rows staged
+                                           through LDS (0)                       */
+};
+
 /* Number of GPUs the library can use (0 without a GPU).  A node process
  * spreads its batches over them, one ctx per device per host thread
  * (block-index partition, no collective). */
@@ -97,6 +142,11 @@ int memo_ec_device_count(void);
 /* Context on GPU `device` (its own HIP stream, device scratch). */
 int memo_ec_ctx_create(int device, memo_ec_ctx **out);
 int memo_ec_ctx_destroy(memo_ec_ctx *ctx);
+
+/* Set / read one memo_ec_option of a ctx (the ctx's owner thread only).
+ * MEMO_EC_EINVAL for an unknown option or a value out of its range. */
+int memo_ec_ctx_set_option(memo_ec_ctx *ctx, int option, int64_t value);
+int memo_ec_ctx_get_option(memo_ec_ctx *ctx, int option, int64_t *value);
 
 /* Enqueue MEMO_EC_DEVICE work on `hip_stream` (a hipStream_t; NULL restores
  * the ctx's own stream).  Lets a caller time kernels with its own events. */
@@ -166,6 +216,23 @@ int memo_ec_decode_rows(memo_ec_ctx *ctx, int k, int m, size_t n,
 int memo_ec_encode_segments(memo_ec_ctx *ctx, int nseg,
                             const memo_ec_segment *segs);
 
+/* Rebuild of up to MEMO_EC_MAX_REBUILD_SEGMENTS groups with different
+ * (k, m, S, e) and per-block or shared erasure patterns in ONE call: the
+ * read side of the multi-address fetch, which hands a whole batch of blocks
+ * over at once (Consensus::_fetch(vector<AddressVersion>, ReceiveBlock),
+ * src/memo/model/doughnut/Consensus.cc:101-124; Paxos::_fetch,
+ * src/memo/model/doughnut/consensus/Paxos.cc:1857-1890).  Segments of one
+ * shard-chunk class and kind share a launch (per-block patterns: the fused
+ * kernel or decode rows + MAC; shared patterns: product tables formed once
+ * on the host), classes run back to back.  Every segment is validated, and
+ * every shared pattern decoded, before anything is enqueued (a bad shared
+ * pattern: MEMO_EC_ESINGULAR).  MEMO_EC_DEVICE: asynchronous on the ctx
+ * stream, per-block faults at memo_ec_synchronize; host memory: synchronous
+ * through the copy pipeline, per-block faults returned (the other blocks
+ * are still rebuilt). */
+int memo_ec_rebuild_segments(memo_ec_ctx *ctx, int nseg,
+                             const memo_ec_rebuild_segment *segs, int where);
+
 /* Batched SHA-256 (FIPS 180-4): digest_i = SHA-256(prefix_i || msg_i) for
  * i < n, with prefix_i = prefix + i*prefix_stride (prefix_len bytes; 0 for
  * none) and msg_i = msg + i*msg_stride of msg_len[i] bytes (msg_len == NULL:
@@ -195,6 +262,11 @@ int memo_ec_gather_shards(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
 
 const char *memo_ec_strerror(int code);
 int memo_ec_version(void);
+/* SHA-256 (hex) of the sources this library was built from: include/
+ * memo_ec.h, memo_amd/csrc/ec_kernels.h, ec_kernels.hip and memo_ec.cpp,
+ * concatenated in that order (memo_amd/csrc/Makefile).  Callers compare it
+ * with the sources they ship to prove the loaded kernels are theirs. */
+const char *memo_ec_build_id(void);
 
 #ifdef __cplusplus
 }

@@ -12,22 +12,8 @@
 #ifndef MEMO_EC_MAC_NT
 #define MEMO_EC_MAC_NT 1
 #endif
-#ifndef MEMO_EC_MAC_TABFIRST
-#define MEMO_EC_MAC_TABFIRST 1
-#endif
 #ifndef MEMO_EC_MAC_W16
 #define MEMO_EC_MAC_W16 1
-#endif
-// 1: shard loads / output stores through buffer resources with the cache
-// policies below (gfx950 cpol: sc0 = 1, nt = 2, sc1 = 16)
-#ifndef MEMO_EC_MAC_BUF
-#define MEMO_EC_MAC_BUF 0
-#endif
-#ifndef MEMO_EC_MAC_LDAUX
-#define MEMO_EC_MAC_LDAUX 2
-#endif
-#ifndef MEMO_EC_MAC_STAUX
-#define MEMO_EC_MAC_STAUX 2
 #endif
 #ifndef MEMO_EC_MAC_PAIR
 #define MEMO_EC_MAC_PAIR 1
@@ -48,12 +34,6 @@
 #define MEMO_EC_MAC_COEF_SOA 1
 #endif
 
-// 1: rebuild table images read from a 5 KiB table of all 256 images in
-// global memory (L1/L2-resident) instead of computed per coefficient
-#ifndef MEMO_EC_MAC_IMGTAB
-#define MEMO_EC_MAC_IMGTAB 0
-#endif
-
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
 #endif
@@ -66,7 +46,6 @@ constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
 constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
 constexpr bool MAC_COEF4 = MEMO_EC_MAC_COEF4 != 0;
 constexpr bool MAC_COEF_SOA = MEMO_EC_MAC_COEF_SOA != 0;
-constexpr bool MAC_IMGTAB = MEMO_EC_MAC_IMGTAB != 0;
 // Table dwords per lane staged through registers ahead of the shard loads.
 constexpr int MAC_TAB_REGS = 2;
 // Coefficients per lane staged through registers (rebuild tables built in
@@ -142,6 +121,10 @@ struct DecodeArgs {
   uint32_t k, m, e;
   uint32_t pitch;         // decode_coef_kernel: LDS row-staging pitch (set by the launcher)
   const uint32_t* lw0;    // LW0 table of (k, m) (lw0_host; 128 bytes); null: computed per workgroup
+  // kernel choice (the ctx's MEMO_EC_OPT_DECODE_* options)
+  uint64_t wide_max;      // batches up to this many blocks: column-per-lane kernel
+  uint32_t exact;         // 1: exact-k kernels for k in {2,3,4,6,8,10,12,14,16}
+  uint32_t stage;         // 1: exact-k rows staged through LDS
 };
 
 struct Sha256Args {

@@ -30,8 +30,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <cstdlib>
-
 #include "ec_kernels.h"
 
 namespace memo_ec {
@@ -122,22 +120,6 @@ __device__ __forceinline__ void st16(uint8_t* p, uint4 v) {
   else *q = w;
 }
 
-// Buffer-resource access (uniform base in SGPRs, 32-bit lane offset, shard
-// offset as the scalar soffset) with an explicit cache policy (gfx950 cpol
-// bits: sc0 = 1, nt = 2, sc1 = 16).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* base) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0xffffffff, 0x00020000);
-}
-__device__ __forceinline__ uint4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
-  const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, MEMO_EC_MAC_LDAUX);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ void bst16(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff,
-                                      uint4 v) {
-  const u32x4 w = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, MEMO_EC_MAC_STAUX);
-}
-
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
@@ -177,13 +159,9 @@ __device__ __forceinline__ Tab read_tab(const TabRef<SOA>& t, uint32_t s) {
 }
 __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl, uint32_t& pm,
                                         uint32_t& ph) {
-#ifdef MEMO_EC_MAC_XORONLY  // diagnostic build: no GF math (wrong results)
-  pl = s.lo ^ t.lo; pm = s.mid; ph = s.hi;
-#else
   pl = __builtin_amdgcn_perm(t.lo, t.lo, s.lo);
   pm = __builtin_amdgcn_perm(t.m1, t.m0, s.mid);
   ph = __builtin_amdgcn_perm(t.h1, t.h0, s.hi);
-#endif
 }
 
 // acc[i] ^= coef(i, j0 + g) * d[g] for the KC shards of one chunk.  Shards
@@ -244,7 +222,6 @@ struct Unit {
   bool valid;
   const uint8_t* pin;
   uint8_t* pout;
-  uint32_t voff_in, voff_out;  // byte offsets from the tile's first block (buffer path)
 };
 
 __device__ __forceinline__ Unit locate(const MacSeg& sg, uint64_t tile) {
@@ -285,8 +262,6 @@ __device__ __forceinline__ Unit locate(const MacSeg& sg, uint64_t tile) {
   const uint64_t b = u.b_first + bo;
   u.pin = sg.in + b * sg.in_bstride + (uint64_t)cc * 16;
   u.pout = sg.out + b * sg.out_bstride + (uint64_t)cc * 16;
-  u.voff_in = (uint32_t)(bo * sg.in_bstride + (uint64_t)cc * 16);
-  u.voff_out = (uint32_t)(bo * sg.out_bstride + (uint64_t)cc * 16);
   return u;
 }
 
@@ -405,32 +380,6 @@ __device__ __forceinline__ void coef_image4(uint32_t c4, uint4 (&q)[4], uint32_t
     q[a] = make_uint4(mid[a], mid[a] ^ bcast_byte(d4, a), hi[a], hi[a] ^ bcast_byte(d7, a));
 }
 
-// The images of all 256 coefficients (q and lo of coef_image), 5 KiB: the
-// rebuild MAC reads a coefficient's image with two loads that hit L1/L2
-// instead of computing it (MAC_IMGTAB).
-struct ImgTable {
-  uint4 q[256];
-  uint32_t lo[256];
-};
-constexpr uint32_t img_xtime(uint32_t x) { return ((x << 1) ^ ((x >> 7) * 0x11Du)) & 0xFFu; }
-constexpr uint32_t img_pack(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  return a | (b << 8) | (c << 16) | (d << 24);
-}
-constexpr ImgTable make_img_table() {
-  ImgTable t{};
-  for (uint32_t c = 0; c < 256; ++c) {
-    uint32_t d[8] = {c, 0, 0, 0, 0, 0, 0, 0};
-    for (int i = 1; i < 8; ++i) d[i] = img_xtime(d[i - 1]);
-    t.q[c].x = img_pack(0, d[2], d[3], d[2] ^ d[3]);
-    t.q[c].y = img_pack(d[4], d[4] ^ d[2], d[4] ^ d[3], d[4] ^ d[3] ^ d[2]);
-    t.q[c].z = img_pack(0, d[5], d[6], d[5] ^ d[6]);
-    t.q[c].w = img_pack(d[7], d[7] ^ d[5], d[7] ^ d[6], d[7] ^ d[6] ^ d[5]);
-    t.lo[c] = img_pack(0, d[0], d[1], d[0] ^ d[1]);
-  }
-  return t;
-}
-__constant__ ImgTable kImg = make_img_table();
-
 // Store the image of slot ci (per = R * kpad slots per set).
 __device__ __forceinline__ void put_image(uint32_t* s_tab, const MacSeg& sg, uint32_t per,
                                           uint32_t ci, const uint4& q, uint32_t lo) {
@@ -483,20 +432,7 @@ __device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
                                              const uint32_t (&cv)[MAC_COEF_REGS], uint32_t* s_tab) {
   const uint32_t total = coef_sets(sg, u) * (R * KP);
   const uint32_t t = threadIdx.x;
-  if constexpr (MAC_IMGTAB) {
-    if (t < total) {  // waves past the tile's slots skip the build
-      uint4 q[MAC_COEF_REGS];
-      uint32_t lo[MAC_COEF_REGS];
-#pragma unroll
-      for (int a = 0; a < MAC_COEF_REGS; ++a) {
-        q[a] = kImg.q[cv[a] & 0xFFu];
-        lo[a] = kImg.lo[cv[a] & 0xFFu];
-      }
-#pragma unroll
-      for (int a = 0; a < MAC_COEF_REGS; ++a)
-        if (t + 256u * a < total) put_image(s_tab, sg, R * KP, t + 256u * a, q[a], lo[a]);
-    }
-  } else if constexpr (MAC_COEF4) {
+  if constexpr (MAC_COEF4) {
     static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
     if (t < total) {  // waves past the tile's slots skip the build
       uint4 q[4];
@@ -969,28 +905,14 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
     // Hot path.  The table image loads go out first (vmcnt retires in issue
     // order, so the LDS copy then waits only for them), the KC shard loads
     // right behind; the barrier and table copy overlap the shard loads.
-#if MEMO_EC_MAC_TABFIRST
     uint32_t tv[COEF ? MAC_COEF_REGS : MAC_TAB_REGS];
     if constexpr (COEF) load_coefs<R, KC>(sg, u, tv);
     else load_tables(sg, u, set_dw, tv);
     uint4 d[KC];
-#if MEMO_EC_MAC_BUF
-    const __amdgpu_buffer_rsrc_t rin = rsrc_of(sg.in + u.b_first * sg.in_bstride);
-#pragma unroll
-    for (int g = 0; g < KC; ++g) d[g] = bld16(rin, u.voff_in, (uint32_t)(g * sg.in_sstride));
-#else
 #pragma unroll
     for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
-#endif
     if constexpr (COEF) store_images<R, KC>(sg, u, tv, s_tab);
     else store_tables(sg, u, set_dw, tv, s_tab);
-#else
-    uint4 d[KC];
-#pragma unroll
-    for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.pin + (uint64_t)g * sg.in_sstride);
-    if constexpr (COEF) stage_images<R>(sg, u, s_tab);
-    else stage_tables(sg, u, set_dw, s_tab);
-#endif
     __syncthreads();
     mac_chunk<KC, R>(acc, d, tab, kpad, 0);
   } else {
@@ -1007,20 +929,11 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   }
 
   if (u.valid) {
-#if MEMO_EC_MAC_BUF
-    const __amdgpu_buffer_rsrc_t rout = rsrc_of(sg.out + u.b_first * sg.out_bstride);
-#pragma unroll
-    for (int i = 0; i < R; ++i)
-      if ((uint32_t)i < sg.r)
-        bst16(rout, u.voff_out, (uint32_t)(i * sg.out_sstride),
-              make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
-#else
 #pragma unroll
     for (int i = 0; i < R; ++i)
       if ((uint32_t)i < sg.r)
         st16<NT>(u.pout + (uint64_t)i * sg.out_sstride,
                  make_uint4(acc[i][0], acc[i][1], acc[i][2], acc[i][3]));
-#endif
   }
 }
 
@@ -1860,18 +1773,12 @@ hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid
   }
 }
 
-// Largest batch that takes the column-per-lane decode (MEMO_EC_DECODE_WIDE_MAX
-// overrides, read per call: tuning and tests).
-static uint64_t decode_wide_max_blocks() {
-  const char* p = std::getenv("MEMO_EC_DECODE_WIDE_MAX");
-  return p ? std::strtoull(p, nullptr, 10) : (uint64_t)65536;
-}
-
 hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   DecodeArgs a = a0;
   if (a.n == 0) return hipSuccess;
-  // Small batches are latency-bound: one lane per survivor column.
-  if (a.n <= decode_wide_max_blocks()) {
+  // Small batches are latency-bound: one lane per survivor column
+  // (a.wide_max: the ctx's MEMO_EC_OPT_DECODE_WIDE_MAX).
+  if (a.n <= a.wide_max) {
     const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
     const uint32_t g = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
     switch (L) {
@@ -1891,14 +1798,10 @@ hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   a.pitch = 256u * pw * 4 <= 64 * 1024 ? pw * 4 : 0u;
   const size_t lds = a.pitch ? 256u * a.pitch : 0;
   // exact-k kernels for the common codes, k in {2, 3, 4, 6, 8, 10, 12, 14,
-  // 16} (MEMO_EC_DECODE_EXACT=0: off; read
-  // per call, for A/B runs and tests)
-  const char* ex_env = std::getenv("MEMO_EC_DECODE_EXACT");
-  const bool exact = !ex_env || std::atoi(ex_env) != 0;
-  // exact-k kernels store whole-dword rows straight from registers
-  // (MEMO_EC_DECODE_STAGE=1: through LDS, for A/B runs)
-  const char* st_env = std::getenv("MEMO_EC_DECODE_STAGE");
-  const bool stage = st_env && std::atoi(st_env) != 0;
+  // 16} (a.exact), storing whole-dword rows straight from registers unless
+  // a.stage asks for the LDS staging (A/B runs and tests)
+  const bool exact = a.exact != 0;
+  const bool stage = a.stage != 0;
   DecodeArgs ax = a;
   if (!stage && (ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) ax.pitch = 0;
   if (exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32) {

@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -22,8 +23,24 @@
 
 using namespace memo_ec;
 
+// Tuning of one ctx (memo_ec_option; defaults from the environment, read
+// once at memo_ec_ctx_create, so no call reads the environment).
+struct memo_ec_opts {
+  int rebuild_path = -1;                  // -1 auto, 0 decode rows + MAC, 1 fused
+  size_t fused_max_bytes = 64ull << 20;   // auto: fused up to this many survivor bytes
+  size_t zc_max_bytes = 4ull << 20;       // host calls up to this many bytes: zero-copy
+  size_t pipe_bytes = 64ull << 20;        // host pipeline batch
+  int copy_threads = 0;                   // pageable bounce copy threads (0: all)
+  uint64_t max_launch_tiles = 0;          // tiles per MAC launch (0: 31-bit grid)
+  uint64_t xcd_min_tiles = 65536;         // XCD-contiguous order from this many tiles
+  uint64_t decode_wide_max = 65536;       // column-per-lane decode up to this many blocks
+  int decode_exact = 1;
+  int decode_stage = 0;
+};
+
 struct memo_ec_ctx {
   int device = 0;
+  memo_ec_opts opt;
   hipStream_t own = nullptr;      // ctx stream
   hipStream_t stream = nullptr;   // stream MEMO_EC_DEVICE work goes to
   // host pipeline: copy-in / compute / copy-out streams, a ring of kSlots
@@ -52,16 +69,17 @@ struct memo_ec_ctx {
     std::vector<uint8_t> key;  // surv_idx (k) || lost_idx (e)
     uint32_t* dev;
     uint64_t used;
+    uint64_t call;             // API call that last used it (never evicted within it)
   };
   std::vector<PatEntry> pat_tabs;  // cached uniform-rebuild table images
   uint64_t pat_clock = 0;
+  uint64_t call_seq = 0;           // API calls that form pattern tables
   // host pipeline: device slots and pinned bounce buffers
   uint8_t* d_slot[3] = {nullptr, nullptr, nullptr};
   size_t slot_cap = 0;
   uint8_t* h_slot[3] = {nullptr, nullptr, nullptr};
   size_t hslot_cap = 0;
   int deferred = 0;
-  size_t pipe_bytes = 64ull << 20;  // host pipeline batch (MEMO_EC_PIPE_MB)
 };
 
 namespace {
@@ -90,6 +108,101 @@ struct DeviceGuard {
     if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
   }
 };
+
+// Bounds of each memo_ec_option (set_option refuses values outside them).
+bool set_opt(memo_ec_opts& o, int opt, int64_t v) {
+  switch (opt) {
+    case MEMO_EC_OPT_REBUILD_PATH:
+      if (v < -1 || v > 1) return false;
+      o.rebuild_path = (int)v;
+      return true;
+    case MEMO_EC_OPT_FUSED_MAX_BYTES:
+      if (v < 0) return false;
+      o.fused_max_bytes = (size_t)v;
+      return true;
+    case MEMO_EC_OPT_ZERO_COPY_BYTES:
+      if (v < 0) return false;
+      o.zc_max_bytes = (size_t)v;
+      return true;
+    case MEMO_EC_OPT_PIPE_BYTES:
+      if (v < (1 << 20) || v > (int64_t(4096) << 20)) return false;
+      o.pipe_bytes = (size_t)v;
+      return true;
+    case MEMO_EC_OPT_COPY_THREADS:
+      if (v < 0 || v > 256) return false;
+      o.copy_threads = (int)v;
+      return true;
+    case MEMO_EC_OPT_MAX_LAUNCH_TILES:
+      if (v < 0) return false;
+      o.max_launch_tiles = (uint64_t)v;
+      return true;
+    case MEMO_EC_OPT_XCD_MIN_TILES:
+      if (v < 0) return false;
+      o.xcd_min_tiles = (uint64_t)v;
+      return true;
+    case MEMO_EC_OPT_DECODE_WIDE_MAX:
+      if (v < 0) return false;
+      o.decode_wide_max = (uint64_t)v;
+      return true;
+    case MEMO_EC_OPT_DECODE_EXACT:
+      if (v < 0 || v > 1) return false;
+      o.decode_exact = (int)v;
+      return true;
+    case MEMO_EC_OPT_DECODE_STAGE:
+      if (v < 0 || v > 1) return false;
+      o.decode_stage = (int)v;
+      return true;
+    default:
+      return false;
+  }
+}
+
+bool get_opt(const memo_ec_opts& o, int opt, int64_t* v) {
+  switch (opt) {
+    case MEMO_EC_OPT_REBUILD_PATH: *v = o.rebuild_path; return true;
+    case MEMO_EC_OPT_FUSED_MAX_BYTES: *v = (int64_t)o.fused_max_bytes; return true;
+    case MEMO_EC_OPT_ZERO_COPY_BYTES: *v = (int64_t)o.zc_max_bytes; return true;
+    case MEMO_EC_OPT_PIPE_BYTES: *v = (int64_t)o.pipe_bytes; return true;
+    case MEMO_EC_OPT_COPY_THREADS: *v = o.copy_threads; return true;
+    case MEMO_EC_OPT_MAX_LAUNCH_TILES: *v = (int64_t)o.max_launch_tiles; return true;
+    case MEMO_EC_OPT_XCD_MIN_TILES: *v = (int64_t)o.xcd_min_tiles; return true;
+    case MEMO_EC_OPT_DECODE_WIDE_MAX: *v = (int64_t)o.decode_wide_max; return true;
+    case MEMO_EC_OPT_DECODE_EXACT: *v = o.decode_exact; return true;
+    case MEMO_EC_OPT_DECODE_STAGE: *v = o.decode_stage; return true;
+    default: return false;
+  }
+}
+
+// Defaults of a new ctx from the environment (once per memo_ec_ctx_create;
+// unparsable or out-of-range values are ignored).
+void read_env_options(memo_ec_opts& o) {
+  struct Env {
+    const char* name;
+    int opt;
+    int shift;  // value << shift (MB / KB variables)
+  };
+  static const Env kEnv[] = {
+      {"MEMO_EC_REBUILD_FUSED", MEMO_EC_OPT_REBUILD_PATH, 0},
+      {"MEMO_EC_FUSED_MAX_MB", MEMO_EC_OPT_FUSED_MAX_BYTES, 20},
+      {"MEMO_EC_ZC_KB", MEMO_EC_OPT_ZERO_COPY_BYTES, 10},
+      {"MEMO_EC_PIPE_MB", MEMO_EC_OPT_PIPE_BYTES, 20},
+      {"MEMO_EC_COPY_THREADS", MEMO_EC_OPT_COPY_THREADS, 0},
+      {"MEMO_EC_MAX_LAUNCH_TILES", MEMO_EC_OPT_MAX_LAUNCH_TILES, 0},
+      {"MEMO_EC_XCD_MIN_TILES", MEMO_EC_OPT_XCD_MIN_TILES, 0},
+      {"MEMO_EC_DECODE_WIDE_MAX", MEMO_EC_OPT_DECODE_WIDE_MAX, 0},
+      {"MEMO_EC_DECODE_EXACT", MEMO_EC_OPT_DECODE_EXACT, 0},
+      {"MEMO_EC_DECODE_STAGE", MEMO_EC_OPT_DECODE_STAGE, 0},
+  };
+  for (const Env& e : kEnv) {
+    const char* p = std::getenv(e.name);
+    if (!p || !*p) continue;
+    char* end = nullptr;
+    const long long v = std::strtoll(p, &end, 10);
+    if (end == p) continue;
+    if (v > (LLONG_MAX >> e.shift) || v < -(LLONG_MAX >> e.shift)) continue;
+    (void)set_opt(o, e.opt, (int64_t)v * ((int64_t)1 << e.shift));
+  }
+}
 
 int check_km(int k, int m) {
   if (k < 1 || m < 0) return MEMO_EC_EINVAL;
@@ -171,10 +284,6 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   return p;
 }
 
-// Launch 1..MEMO_EC_MAX_SEGMENTS planned segments as one kernel, one tile
-// per workgroup.  All share KC and R (the common compile-time bounds).
-// Smallest segment (in tiles) that gets the XCD-contiguous order;
-// MEMO_EC_XCD_MIN_TILES overrides (tuning).
 // Largest table LDS of a launch's segments.
 size_t lds_of(const std::vector<Plan>& plans) {
   size_t lds = 0;
@@ -182,39 +291,41 @@ size_t lds_of(const std::vector<Plan>& plans) {
   return lds;
 }
 
-uint64_t xcd_min_tiles() {
-  static const uint64_t v = [] {
-    const char* p = std::getenv("MEMO_EC_XCD_MIN_TILES");
-    return p ? std::strtoull(p, nullptr, 10) : (uint64_t)65536;
-  }();
-  return v;
-}
-
-int launch_plans(std::vector<Plan>& plans, hipStream_t st) {
+// Launch planned segments that share KC, R and mode, one tile per
+// workgroup: MEMO_EC_MAX_SEGMENTS segments (and < 2^31 workgroups) per
+// kernel launch, more segments in further launches back to back.
+int launch_plans(const memo_ec_ctx* c, std::vector<Plan>& plans, hipStream_t st) {
   if (plans.empty()) return MEMO_EC_OK;
-  MacLaunch L{};
-  L.nseg = 0;
-  uint64_t wg = 0;
-  size_t lds = 0;
   const int KC = plans[0].KC, R = plans[0].R, mode = plans[0].mode;
-  for (auto& p : plans) {
+  for (const auto& p : plans)
     if (p.KC != KC || p.R != R || p.mode != mode) return MEMO_EC_EINVAL;
-    if (p.seg.tiles == 0) continue;
-    wg = (wg + 7) / 8 * 8;  // segments start on an XCD-round boundary
-    p.seg.wg_begin = (uint32_t)wg;
-    wg += p.seg.tiles;
-    lds = std::max(lds, p.lds);
-    L.seg[L.nseg++] = p.seg;
+  if (lds_of(plans) > 160 * 1024) return MEMO_EC_ERANGE;
+  size_t i = 0;
+  while (i < plans.size()) {
+    MacLaunch L{};
+    L.nseg = 0;
+    uint64_t wg = 0;
+    size_t lds = 0;
+    for (; i < plans.size() && L.nseg < MEMO_EC_MAX_SEGMENTS; ++i) {
+      Plan& p = plans[i];
+      if (p.seg.tiles == 0) continue;
+      const uint64_t begin = (wg + 7) / 8 * 8;  // segments start on an XCD-round boundary
+      if (L.nseg && begin + p.seg.tiles > 0x7fffffffull) break;  // next launch
+      p.seg.wg_begin = (uint32_t)begin;
+      wg = begin + p.seg.tiles;
+      lds = std::max(lds, p.lds);
+      L.seg[L.nseg++] = p.seg;
+    }
+    if (wg == 0) continue;
+    if (wg > 0x7fffffffull) return MEMO_EC_ERANGE;
+    // The XCD-contiguous tile order pays on large grids (C2, 105k
+    // workgroups: +4%) and costs a few % on grids of a few 10k.
+    uint64_t min_tiles = ~0ull;
+    for (uint32_t s = 0; s < L.nseg; ++s) min_tiles = std::min<uint64_t>(min_tiles, L.seg[s].tiles);
+    L.xcd = min_tiles >= c->opt.xcd_min_tiles ? 1u : 0u;
+    if (int rc = hip_rc(launch_mac(KC, R, mode, L, (uint32_t)wg, lds, st))) return rc;
   }
-  if (wg == 0) return MEMO_EC_OK;
-  if (wg > 0x7fffffffull) return MEMO_EC_ERANGE;
-  // The XCD-contiguous tile order pays on large grids (C2, 105k workgroups:
-  // +4%) and costs a few % on grids of a few 10k.
-  uint64_t min_tiles = ~0ull;
-  for (uint32_t i = 0; i < L.nseg; ++i) min_tiles = std::min<uint64_t>(min_tiles, L.seg[i].tiles);
-  L.xcd = min_tiles >= xcd_min_tiles() ? 1u : 0u;
-  if (lds > 160 * 1024) return MEMO_EC_ERANGE;
-  return hip_rc(launch_mac(KC, R, mode, L, (uint32_t)wg, lds, st));
+  return MEMO_EC_OK;
 }
 
 // Cached device table image of the Cauchy parity rows of (k, m).
@@ -272,12 +383,10 @@ int lw0_table(memo_ec_ctx* ctx, int k, int m, const uint32_t** out) {
 //    gf_mac_kernel) above: the MAC is ~75% VALU-busy and the fused decode's
 //    VALU/LDS work costs more than the decode kernel it removes (C3 1054 vs
 //    1012 us, 4 KiB RS(10,4) 1239 vs 1186 us, profiles/r02_rebuild_pmc.md).
-// MEMO_EC_REBUILD_FUSED=0/1 forces one path (read per call: A/B and tests).
-bool rebuild_fused(size_t in_bytes) {
-  if (const char* p = std::getenv("MEMO_EC_REBUILD_FUSED")) return std::atoi(p) != 0;
-  size_t max_mb = 64;
-  if (const char* p = std::getenv("MEMO_EC_FUSED_MAX_MB")) max_mb = std::strtoull(p, nullptr, 10);
-  return in_bytes <= (max_mb << 20);
+// MEMO_EC_OPT_REBUILD_PATH 0/1 forces one path (A/B runs and tests).
+bool rebuild_fused(const memo_ec_ctx* c, size_t in_bytes) {
+  if (c->opt.rebuild_path >= 0) return c->opt.rebuild_path != 0;
+  return in_bytes <= c->opt.fused_max_bytes;
 }
 
 int sync_pipeline(memo_ec_ctx* ctx);
@@ -306,19 +415,18 @@ constexpr int kSlots = 3;
 // moves ~10-20 GB/s, below the ~50 GB/s a PCIe Gen5 x16 direction carries.
 // The workers are shared by every ctx of the process and started once; the
 // calling thread copies a chunk too and helps with queued chunks while it
-// waits.  MEMO_EC_COPY_THREADS (read per call) caps the threads per copy;
-// 1 copies on the calling thread only.
+// waits.  `threads` (the ctx's MEMO_EC_OPT_COPY_THREADS; 0: no cap) caps the
+// threads per copy; 1 copies on the calling thread only.
 class CopyPool {
  public:
   static CopyPool& get() {
     static CopyPool* p = new CopyPool();  // never destroyed: workers may be blocked at exit
     return *p;
   }
-  void copy(void* dst, const void* src, size_t n) {
+  void copy(void* dst, const void* src, size_t n, int threads) {
     constexpr size_t kChunkMin = 128u << 10;
     size_t nt = std::min<size_t>(workers_ + 1, n / kChunkMin);
-    if (const char* p = std::getenv("MEMO_EC_COPY_THREADS"))
-      nt = std::min<size_t>(nt, (size_t)std::max(1L, std::strtol(p, nullptr, 10)));
+    if (threads > 0) nt = std::min<size_t>(nt, (size_t)threads);
     if (nt <= 1) {
       std::memcpy(dst, src, n);
       return;
@@ -392,7 +500,9 @@ class CopyPool {
   std::vector<Chunk> q_;
 };
 
-void par_memcpy(void* dst, const void* src, size_t n) { CopyPool::get().copy(dst, src, n); }
+void par_memcpy(const memo_ec_ctx* c, void* dst, const void* src, size_t n) {
+  CopyPool::get().copy(dst, src, n, c->opt.copy_threads);
+}
 
 int sync_pipeline(memo_ec_ctx* ctx) {
   for (auto st : {ctx->sh, ctx->sk, ctx->sd}) HIPCHK(hipStreamSynchronize(st));
@@ -429,22 +539,16 @@ int ensure_slots(memo_ec_ctx* ctx, size_t dev_bytes, size_t host_bytes) {
 // kernels on pinned host memory directly, with no DMA copies: 5-40% less
 // time than the copy pipeline up to ~8 MiB of input, more beyond, where the
 // pipeline's copy overlap and threaded bounce copies win
-// (profiles/r01_zero_copy_probe.jsonl).  MEMO_EC_ZC_KB overrides (read per
-// call; 0 disables).
-size_t zc_max_bytes() {
-  const char* p = std::getenv("MEMO_EC_ZC_KB");
-  return p ? (size_t)std::strtoull(p, nullptr, 10) << 10 : (size_t)4 << 20;
-}
+// (profiles/r01_zero_copy_probe.jsonl).  The ctx's MEMO_EC_OPT_ZERO_COPY_BYTES
+// (0 disables).
+size_t zc_max_bytes(const memo_ec_ctx* c) { return c->opt.zc_max_bytes; }
 
 // Largest batch (blocks) one MAC launch takes: tiles must fit a 31-bit grid.
-// MEMO_EC_MAX_LAUNCH_TILES lowers the bound so tests can reach the split
+// MEMO_EC_OPT_MAX_LAUNCH_TILES lowers the bound so tests can reach the split
 // path without a 2^31-tile batch.
-size_t max_blocks_per_launch(size_t S) {
+size_t max_blocks_per_launch(const memo_ec_ctx* c, size_t S) {
   uint64_t limit = 0x7fffffffull - MAC_TILE;
-  if (const char* p = std::getenv("MEMO_EC_MAX_LAUNCH_TILES")) {
-    const uint64_t v = std::strtoull(p, nullptr, 10);
-    if (v >= 1 && v < limit) limit = v;
-  }
+  if (c->opt.max_launch_tiles >= 1 && c->opt.max_launch_tiles < limit) limit = c->opt.max_launch_tiles;
   const uint64_t per = (S / 16 + MAC_TILE - 1) / MAC_TILE + 1;
   return (size_t)std::max<uint64_t>(1, limit / per);
 }
@@ -455,16 +559,35 @@ int encode_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint
   const int R = mac_rbound(m), KC = mac_kchunk(k, R);
   const uint32_t* tab = nullptr;
   if (int rc = encode_tables(ctx, k, m, R, KC, &tab)) return rc;
-  const size_t step = max_blocks_per_launch(S);
+  const size_t step = max_blocks_per_launch(ctx, S);
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
     std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)m, S, cnt,
                                          data + b0 * (size_t)k * S, (uint64_t)k * S, S,
                                          parity + b0 * (size_t)m * S, (uint64_t)m * S, S, tab, 0,
                                          KC, R)};
-    if (int rc = launch_plans(plans, st)) return rc;
+    if (int rc = launch_plans(ctx, plans, st)) return rc;
   }
   return MEMO_EC_OK;
+}
+
+DecodeArgs decode_args(const memo_ec_ctx* c, int k, int m, int e, size_t n, const uint8_t* surv_idx,
+                       const uint8_t* lost_idx, uint8_t* rows, uint32_t* status, const uint32_t* lw0) {
+  DecodeArgs a{};
+  a.surv_idx = surv_idx;
+  a.lost_idx = lost_idx;
+  a.rows = rows;
+  a.status = status;
+  a.n = n;
+  a.k = (uint32_t)k;
+  a.m = (uint32_t)m;
+  a.e = (uint32_t)e;
+  a.pitch = 0;
+  a.lw0 = lw0;
+  a.wide_max = c->opt.decode_wide_max;
+  a.exact = c->opt.decode_exact ? 1u : 0u;
+  a.stage = c->opt.decode_stage ? 1u : 0u;
+  return a;
 }
 
 // Device-resident rebuild on stream st.  Fused (default): one launch of
@@ -476,7 +599,7 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
                    bool fused, void* scratch, hipStream_t st, uint32_t* status) {
   const int R = mac_rbound(e), KC = mac_kchunk(k, R);
-  const size_t step = max_blocks_per_launch(S);
+  const size_t step = max_blocks_per_launch(ctx, S);
   if (fused) {
     const uint32_t* lw0 = nullptr;
     if (int rc = lw0_table(ctx, k, m, &lw0)) return rc;
@@ -491,7 +614,7 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
       p.seg.status = status;
       p.seg.m = (uint32_t)m;
       std::vector<Plan> plans{p};
-      if (int rc = launch_plans(plans, st)) return rc;
+      if (int rc = launch_plans(ctx, plans, st)) return rc;
     }
     return MEMO_EC_OK;
   }
@@ -499,7 +622,7 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
   const uint64_t row_b = (uint64_t)e * k;
   const uint32_t* lw0 = nullptr;
   if (int rc = lw0_table(ctx, k, m, &lw0)) return rc;
-  DecodeArgs a{surv_idx, lost_idx, rows, status, n, (uint32_t)k, (uint32_t)m, (uint32_t)e, 0, lw0};
+  const DecodeArgs a = decode_args(ctx, k, m, e, n, surv_idx, lost_idx, rows, status, lw0);
   HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
@@ -508,7 +631,7 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
                                          out + b0 * (size_t)e * S, (uint64_t)e * S, S,
                                          nullptr, 0, KC, R, rows + b0 * row_b, row_b,
                                          (uint32_t)e)};
-    if (int rc = launch_plans(plans, st)) return rc;
+    if (int rc = launch_plans(ctx, plans, st)) return rc;
   }
   return MEMO_EC_OK;
 }
@@ -522,50 +645,70 @@ size_t tab_bytes(int k, int e, size_t n, bool fused) { return fused ? 0 : n * (s
 // call itself) each have their own, so neither consumes the other's fault.
 constexpr size_t kStatusDevice = 0, kStatusPipeline = 16;
 
-// Host-memory pipeline over batches of nb blocks.  Batch i uses slot i % 3:
-//   in(slot, b0, cnt, st)   host staging + HtoD copies on st
-//   run(slot, b0, cnt, st)  kernels on st, after the slot's HtoD
-//   out(slot, b0, cnt, st)  DtoH copies on st, after the kernels
-//   done(slot, b0, cnt)     host side after the DtoH (pageable copy-out)
-// With several batches the three stages run on the copy-in, compute and
-// copy-out streams chained by events, so the HtoD of batch i+1 runs under
-// the DtoH of batch i (PCIe duplex).  A single batch has nothing to overlap
+// Host-memory pipeline over nw waves.  Wave w uses slot w % 3:
+//   in(slot, w, st)    host staging + HtoD copies on st
+//   run(slot, w, st)   kernels on st, after the slot's HtoD
+//   out(slot, w, st)   DtoH copies on st, after the kernels
+//   done(slot, w)      host side after the DtoH (pageable copy-out)
+// With several waves the three stages run on the copy-in, compute and
+// copy-out streams chained by events, so the HtoD of wave i+1 runs under
+// the DtoH of wave i (PCIe duplex).  A single wave has nothing to overlap
 // and runs on one stream, without the cross-stream event hops (latency).
 template <class In, class Run, class Out, class Done>
-int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, Done done) {
-  size_t off[kSlots] = {}, cnt[kSlots] = {};
-  const size_t nbatch = (n + nb - 1) / nb;
-  const bool one = nbatch == 1;
+int run_waves(memo_ec_ctx* c, size_t nw, In in, Run run, Out out, Done done) {
+  size_t wave[kSlots] = {};
+  bool busy[kSlots] = {};
+  const bool one = nw == 1;
   hipStream_t s_in = one ? c->sk : c->sh, s_out = one ? c->sk : c->sd;
   auto finish = [&](int s) -> int {
-    if (!cnt[s]) return MEMO_EC_OK;
+    if (!busy[s]) return MEMO_EC_OK;
     HIPCHK(hipEventSynchronize(c->ev_d[s]));
-    done(s, off[s], cnt[s]);
-    cnt[s] = 0;
+    done(s, wave[s]);
+    busy[s] = false;
     return MEMO_EC_OK;
   };
-  for (size_t bi = 0; bi < nbatch; ++bi) {
-    const int s = (int)(bi % kSlots);
+  for (size_t w = 0; w < nw; ++w) {
+    const int s = (int)(w % kSlots);
     if (int rc = finish(s)) return rc;
-    const size_t b0 = bi * nb, cn = std::min(nb, n - b0);
-    if (int rc = in(s, b0, cn, s_in)) return rc;
+    if (int rc = in(s, w, s_in)) return rc;
     if (!one) {
       HIPCHK(hipEventRecord(c->ev_h[s], c->sh));
       HIPCHK(hipStreamWaitEvent(c->sk, c->ev_h[s], 0));
     }
-    if (int rc = run(s, b0, cn, c->sk)) return rc;
+    if (int rc = run(s, w, c->sk)) return rc;
     if (!one) {
       HIPCHK(hipEventRecord(c->ev_k[s], c->sk));
       HIPCHK(hipStreamWaitEvent(c->sd, c->ev_k[s], 0));
     }
-    if (int rc = out(s, b0, cn, s_out)) return rc;
+    if (int rc = out(s, w, s_out)) return rc;
     HIPCHK(hipEventRecord(c->ev_d[s], s_out));
-    off[s] = b0;
-    cnt[s] = cn;
+    wave[s] = w;
+    busy[s] = true;
   }
-  for (size_t bi = nbatch > kSlots ? nbatch - kSlots : 0; bi < nbatch; ++bi)
-    if (int rc = finish((int)(bi % kSlots))) return rc;
+  for (size_t w = nw > kSlots ? nw - kSlots : 0; w < nw; ++w)
+    if (int rc = finish((int)(w % kSlots))) return rc;
   return MEMO_EC_OK;
+}
+
+// run_waves over batches of nb of n blocks: the callbacks get (slot, first
+// block, blocks[, stream]).
+template <class In, class Run, class Out, class Done>
+int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, Done done) {
+  auto span = [&](size_t w, size_t& b0, size_t& cn) {
+    b0 = w * nb;
+    cn = std::min(nb, n - b0);
+  };
+  size_t b0, cn;
+  return run_waves(
+      c, (n + nb - 1) / nb,
+      [&](int s, size_t w, hipStream_t st) { span(w, b0, cn); return in(s, b0, cn, st); },
+      [&](int s, size_t w, hipStream_t st) { span(w, b0, cn); return run(s, b0, cn, st); },
+      [&](int s, size_t w, hipStream_t st) { span(w, b0, cn); return out(s, b0, cn, st); },
+      [&](int s, size_t w) {
+        size_t x0, xn;
+        span(w, x0, xn);
+        done(s, x0, xn);
+      });
 }
 
 // A host-memory call of one multiply-accumulate over n blocks of in_b bytes
@@ -576,23 +719,23 @@ int run_pipeline(memo_ec_ctx* c, size_t n, size_t nb, In in, Run run, Out out, D
 template <class Run>
 int host_mac(memo_ec_ctx* c, size_t n, size_t in_b, size_t out_b, const uint8_t* data,
              uint8_t* out, bool pinned, Run run) {
-  if (n * (in_b + out_b) <= zc_max_bytes()) {
+  if (n * (in_b + out_b) <= zc_max_bytes(c)) {
     // Small call: the kernel reads the blocks from, and writes its output
     // to, pinned host memory over PCIe -- no DMA copies to wait for.
     if (int rc = ensure_slots(c, 0, pinned ? 0 : n * (in_b + out_b))) return rc;
     const uint8_t* src = data;
     uint8_t* dst = out;
     if (!pinned) {
-      par_memcpy(c->h_slot[0], data, n * in_b);
+      par_memcpy(c, c->h_slot[0], data, n * in_b);
       src = c->h_slot[0];
       dst = c->h_slot[0] + n * in_b;
     }
     if (int rc = run(src, dst, n, c->sk)) return rc;
     HIPCHK(hipStreamSynchronize(c->sk));
-    if (!pinned) par_memcpy(out, dst, n * out_b);
+    if (!pinned) par_memcpy(c, out, dst, n * out_b);
     return MEMO_EC_OK;
   }
-  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
+  size_t nb = std::max<size_t>(1, c->opt.pipe_bytes / in_b);
   nb = std::min(nb, n);
   if (int rc = ensure_slots(c, nb * (in_b + out_b), pinned ? 0 : nb * (in_b + out_b))) return rc;
   // slot layout (device and pageable bounce): [in nb*in_b | out nb*out_b]
@@ -601,7 +744,7 @@ int host_mac(memo_ec_ctx* c, size_t n, size_t in_b, size_t out_b, const uint8_t*
       [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         const uint8_t* src = data + b0 * in_b;
         if (!pinned) {
-          par_memcpy(c->h_slot[s], src, cnt * in_b);
+          par_memcpy(c, c->h_slot[s], src, cnt * in_b);
           src = c->h_slot[s];
         }
         return hip_rc(hipMemcpyAsync(c->d_slot[s], src, cnt * in_b, hipMemcpyHostToDevice, st));
@@ -615,7 +758,7 @@ int host_mac(memo_ec_ctx* c, size_t n, size_t in_b, size_t out_b, const uint8_t*
                                      hipMemcpyDeviceToHost, st));
       },
       [&](int s, size_t b0, size_t cnt) {
-        if (!pinned) par_memcpy(out + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
+        if (!pinned) par_memcpy(c, out + b0 * out_b, c->h_slot[s] + nb * in_b, cnt * out_b);
       });
 }
 
@@ -677,6 +820,7 @@ int pattern_tables(memo_ec_ctx* ctx, int k, int m, const uint8_t* sidx, const ui
   for (auto& p : ctx->pat_tabs)
     if (p.k == k && p.m == m && p.R == R && p.kpad == kpad && p.key == key) {
       p.used = ctx->pat_clock;
+      p.call = ctx->call_seq;
       *out = p.dev;
       return MEMO_EC_OK;
     }
@@ -684,12 +828,16 @@ int pattern_tables(memo_ec_ctx* ctx, int k, int m, const uint8_t* sidx, const ui
   if (!host_decode_rows(k, m, sidx, lidx, e, rows.data())) return MEMO_EC_ESINGULAR;
   std::vector<uint32_t> img((size_t)R * kpad * 8);
   table_image_host(rows.data(), (uint32_t)e, (uint32_t)k, (uint32_t)R, (uint32_t)kpad, img.data());
-  if (ctx->pat_tabs.size() >= 64) {
+  // past 64 images the least recently used goes, unless the current call
+  // (a rebuild_segments call with many patterns) still needs it
+  auto lru = ctx->pat_tabs.end();
+  if (ctx->pat_tabs.size() >= 64)
+    for (auto it = ctx->pat_tabs.begin(); it != ctx->pat_tabs.end(); ++it)
+      if (it->call != ctx->call_seq && (lru == ctx->pat_tabs.end() || it->used < lru->used)) lru = it;
+  if (lru != ctx->pat_tabs.end()) {
     // the evicted image may still be read by enqueued work on this ctx
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (int rc = sync_pipeline(ctx)) return rc;
-    auto lru = std::min_element(ctx->pat_tabs.begin(), ctx->pat_tabs.end(),
-                                [](const auto& a, const auto& b) { return a.used < b.used; });
     HIPCHK(hipFree(lru->dev));
     ctx->pat_tabs.erase(lru);
   }
@@ -700,8 +848,158 @@ int pattern_tables(memo_ec_ctx* ctx, int k, int m, const uint8_t* sidx, const ui
     (void)hipFree(dev);
     return hip_rc(err);
   }
-  ctx->pat_tabs.push_back({k, m, R, kpad, std::move(key), dev, ctx->pat_clock});
+  ctx->pat_tabs.push_back({k, m, R, kpad, std::move(key), dev, ctx->pat_clock, ctx->call_seq});
   *out = dev;
+  return MEMO_EC_OK;
+}
+
+// ---- Mixed-geometry rebuild (memo_ec_rebuild_segments).
+// A piece: blocks [b0, b0 + n) of one segment, with the pointers the
+// kernels read (device memory, or pinned host memory for a zero-copy call)
+// and its launch class, fixed once per call: shard chunk KC, row bound R
+// (the class's largest), mode (MAC_ENCODE for a shared pattern, whose
+// product tables `tab` were formed on the host; MAC_FUSED or MAC_ROWS for
+// per-block patterns).
+struct RPiece {
+  int seg = 0;
+  int k = 0, m = 0, e = 0;
+  size_t S = 0, n = 0, b0 = 0;
+  const uint8_t* sidx = nullptr;  // per-block: n x k
+  const uint8_t* surv = nullptr;  // n x k x S
+  const uint8_t* lidx = nullptr;  // per-block: n x e
+  uint8_t* out = nullptr;         // n x e x S
+  int mode = MAC_ENCODE, KC = 4, R = 1;
+  const uint32_t* tab = nullptr;  // shared pattern: table image
+};
+
+// Decode-row bytes the pieces of MAC_ROWS classes need.
+size_t rows_bytes(const std::vector<RPiece>& ps) {
+  size_t b = 0;
+  for (const auto& p : ps)
+    if (p.mode == MAC_ROWS) b += p.n * (size_t)p.e * p.k;
+  return b;
+}
+
+// Validates the segments and assigns each non-empty one its class:
+// pieces[i] describes segment i whole (pointers as the caller gave them).
+// Shared patterns are decoded (and their tables cached) here, before
+// anything is enqueued.
+int plan_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segment* segs,
+                          std::vector<RPiece>& pieces) {
+  pieces.clear();
+  for (int i = 0; i < nseg; ++i) {
+    const auto& s = segs[i];
+    if (int rc = check_km(s.k, s.m)) return rc;
+    if (s.e < 0 || s.e > s.m) return MEMO_EC_EINVAL;
+    if (s.e == 0 || s.n == 0) continue;
+    if (s.S == 0 || s.S % 64 || !s.surv_idx || !s.surv || !s.lost_idx || !s.out) return MEMO_EC_EINVAL;
+    RPiece p;
+    p.seg = i;
+    p.k = s.k;
+    p.m = s.m;
+    p.e = s.e;
+    p.S = s.S;
+    p.n = s.n;
+    p.sidx = s.surv_idx;
+    p.surv = s.surv;
+    p.lidx = s.lost_idx;
+    p.out = s.out;
+    p.R = mac_rbound(s.e);
+    p.KC = mac_kchunk(s.k, p.R);
+    p.mode = s.uniform ? MAC_ENCODE : MAC_ROWS;  // per-block: fused or rows, below
+    pieces.push_back(p);
+  }
+  // classes (kind, KC): R = the class's largest bound.  KC = 6, 12, 14 are
+  // only chosen for R <= 4, so their classes stay within the instantiated
+  // bodies.  Per-block classes take the fused kernel up to the ctx's fused
+  // bound of survivor bytes (as memo_ec_rebuild_batch does per call).
+  struct Cls {
+    bool uniform;
+    int KC, R;
+    size_t in_bytes;
+  };
+  std::vector<Cls> cls;
+  std::vector<size_t> of(pieces.size());
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    const auto& p = pieces[i];
+    const bool u = p.mode == MAC_ENCODE;
+    size_t ci = 0;
+    while (ci < cls.size() && !(cls[ci].uniform == u && cls[ci].KC == p.KC)) ++ci;
+    if (ci == cls.size()) cls.push_back({u, p.KC, 1, 0});
+    cls[ci].R = std::max(cls[ci].R, p.R);
+    cls[ci].in_bytes += p.n * (size_t)p.k * p.S;
+    of[i] = ci;
+  }
+  ++c->call_seq;
+  for (size_t i = 0; i < pieces.size(); ++i) {
+    auto& p = pieces[i];
+    const Cls& k = cls[of[i]];
+    p.R = k.R;
+    if (p.mode == MAC_ENCODE) {
+      if (int rc = pattern_tables(c, p.k, p.m, p.sidx, p.lidx, p.e, p.R, p.KC, &p.tab)) return rc;
+    } else {
+      p.mode = rebuild_fused(c, k.in_bytes) ? MAC_FUSED : MAC_ROWS;
+    }
+  }
+  return MEMO_EC_OK;
+}
+
+// Enqueue the kernels of `ps` on st: decode rows of MAC_ROWS pieces into
+// `rows` (rows_bytes(ps) bytes), then one launch set per (mode, KC, R)
+// class, pieces longer than one launch's grid split by blocks.
+int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t* rows,
+                          hipStream_t st, uint32_t* status) {
+  std::vector<const uint8_t*> prow(ps.size(), nullptr);
+  size_t off = 0;
+  for (size_t i = 0; i < ps.size(); ++i) {
+    const auto& p = ps[i];
+    if (p.mode != MAC_ROWS) continue;
+    const uint32_t* lw0 = nullptr;
+    if (int rc = lw0_table(c, p.k, p.m, &lw0)) return rc;
+    const DecodeArgs a = decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0);
+    HIPCHK(launch_decode_coef(a, st));
+    prow[i] = rows + off;
+    off += p.n * (size_t)p.e * p.k;
+  }
+  std::vector<bool> done(ps.size(), false);
+  for (size_t i = 0; i < ps.size(); ++i) {
+    if (done[i]) continue;
+    const int mode = ps[i].mode, KC = ps[i].KC, R = ps[i].R;
+    std::vector<Plan> plans;
+    for (size_t j = i; j < ps.size(); ++j) {
+      const auto& p = ps[j];
+      if (done[j] || p.mode != mode || p.KC != KC || p.R != R) continue;
+      done[j] = true;
+      const size_t step = max_blocks_per_launch(c, p.S);
+      const uint32_t* lw0 = nullptr;
+      if (mode == MAC_FUSED)
+        if (int rc = lw0_table(c, p.k, p.m, &lw0)) return rc;
+      for (size_t b0 = 0; b0 < p.n; b0 += step) {
+        const size_t cnt = std::min(step, p.n - b0);
+        const uint64_t in_bs = (uint64_t)p.k * p.S, out_bs = (uint64_t)p.e * p.S;
+        const uint8_t* in = p.surv + b0 * in_bs;
+        uint8_t* out = p.out + b0 * out_bs;
+        if (mode == MAC_ENCODE) {
+          plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
+                                       p.S, p.tab, 0, KC, R));
+        } else if (mode == MAC_ROWS) {
+          const uint64_t row_b = (uint64_t)p.e * p.k;
+          plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
+                                       p.S, nullptr, 0, KC, R, prow[j] + b0 * row_b, row_b, (uint32_t)p.e));
+        } else {
+          Plan q = plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs, p.S,
+                                nullptr, 0, KC, R, nullptr, (uint64_t)p.e * p.k, (uint32_t)p.e, true);
+          q.seg.sidx = p.sidx + b0 * (size_t)p.k;
+          q.seg.lidx = p.lidx + b0 * (size_t)p.e;
+          q.seg.lw0 = lw0;
+          q.seg.status = status;
+          q.seg.m = (uint32_t)p.m;
+          plans.push_back(q);
+        }
+      }
+    }
+    if (int rc = launch_plans(c, plans, st)) return rc;
+  }
   return MEMO_EC_OK;
 }
 
@@ -723,6 +1021,21 @@ int take_deferred(memo_ec_ctx* ctx) {
 extern "C" {
 
 int memo_ec_version(void) { return MEMO_EC_VERSION; }
+
+#ifndef MEMO_EC_BUILD_ID
+#define MEMO_EC_BUILD_ID "unknown"
+#endif
+const char* memo_ec_build_id(void) { return MEMO_EC_BUILD_ID; }
+
+int memo_ec_ctx_set_option(memo_ec_ctx* c, int option, int64_t value) {
+  if (!c) return MEMO_EC_EINVAL;
+  return set_opt(c->opt, option, value) ? MEMO_EC_OK : MEMO_EC_EINVAL;
+}
+
+int memo_ec_ctx_get_option(memo_ec_ctx* c, int option, int64_t* value) {
+  if (!c || !value) return MEMO_EC_EINVAL;
+  return get_opt(c->opt, option, value) ? MEMO_EC_OK : MEMO_EC_EINVAL;
+}
 
 int memo_ec_device_count(void) {
   int n = 0;
@@ -794,10 +1107,7 @@ int memo_ec_ctx_create(int device, memo_ec_ctx** out) {
       return rc;
     }
   }
-  if (const char* p = std::getenv("MEMO_EC_PIPE_MB")) {
-    const long v = std::atol(p);
-    if (v >= 1 && v <= 4096) c->pipe_bytes = (size_t)v << 20;
-  }
+  read_env_options(c->opt);
   c->stream = c->own;
   *out = c;
   return MEMO_EC_OK;
@@ -893,15 +1203,16 @@ int memo_ec_rebuild_uniform(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   DeviceGuard g(c->device);
   const int R = mac_rbound(e), KC = mac_kchunk(k, R);
   const uint32_t* tab = nullptr;
+  ++c->call_seq;
   if (int rc = pattern_tables(c, k, m, surv_idx, lost_idx, e, R, KC, &tab)) return rc;
   auto run = [&](const uint8_t* src, uint8_t* dst, size_t cnt, hipStream_t st) -> int {
-    const size_t step = max_blocks_per_launch(S);
+    const size_t step = max_blocks_per_launch(c, S);
     for (size_t b0 = 0; b0 < cnt; b0 += step) {
       const size_t bc = std::min(step, cnt - b0);
       std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, bc, src + b0 * (size_t)k * S,
                                            (uint64_t)k * S, S, dst + b0 * (size_t)e * S,
                                            (uint64_t)e * S, S, tab, 0, KC, R)};
-      if (int rc = launch_plans(plans, st)) return rc;
+      if (int rc = launch_plans(c, plans, st)) return rc;
     }
     return MEMO_EC_OK;
   };
@@ -920,8 +1231,8 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   DeviceGuard g(c->device);
   const uint32_t* lw0 = nullptr;
   if (int rc = lw0_table(c, k, m, &lw0)) return rc;
-  DecodeArgs a{surv_idx, lost_idx, rows, c->d_status + kStatusDevice, n, (uint32_t)k, (uint32_t)m,
-               (uint32_t)e, 0, lw0};
+  const DecodeArgs a = decode_args(c, k, m, e, n, surv_idx, lost_idx, rows, c->d_status + kStatusDevice,
+                                   lw0);
   return hip_rc(launch_decode_coef(a, c->stream));
 }
 
@@ -934,7 +1245,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
   DeviceGuard g(c->device);
-  const bool fused = rebuild_fused(n * (size_t)k * S);
+  const bool fused = rebuild_fused(c, n * (size_t)k * S);
   if (where == MEMO_EC_DEVICE) {
     if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
     if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, fused, c->d_tabs,
@@ -955,7 +1266,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   } else if (q != hipSuccess) {
     return hip_rc(q);
   }
-  if (n * (in_b + out_b + idx_b) + 4 <= zc_max_bytes()) {
+  if (n * (in_b + out_b + idx_b) + 4 <= zc_max_bytes(c)) {
     // Small call: decode and MAC run on pinned host memory directly (the
     // survivors, indices and output in the bounce slot, or the caller's
     // pinned buffers); the status word rides in the slot too.
@@ -972,7 +1283,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
     const uint8_t* sv = surv;
     uint8_t* ov = out;
     if (!pinned) {
-      par_memcpy(h, surv, n * in_b);
+      par_memcpy(c, h, surv, n * in_b);
       sv = h;
       ov = h + n * in_b;
     }
@@ -980,13 +1291,13 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
                                 h_st))
       return rc;
     HIPCHK(hipStreamSynchronize(c->sk));
-    if (!pinned) par_memcpy(out, ov, n * out_b);
+    if (!pinned) par_memcpy(c, out, ov, n * out_b);
     int drc = c->deferred;
     c->deferred = 0;
     if (drc == MEMO_EC_OK && (__atomic_load_n(h_st, __ATOMIC_ACQUIRE) & 1u)) drc = MEMO_EC_ESINGULAR;
     return drc;
   }
-  size_t nb = std::max<size_t>(1, c->pipe_bytes / in_b);
+  size_t nb = std::max<size_t>(1, c->opt.pipe_bytes / in_b);
   nb = std::min(nb, n);
   // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e]
   const size_t slot = nb * (in_b + out_b + idx_b);
@@ -1004,7 +1315,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
         HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx, nb * idx_b, hipMemcpyHostToDevice, st));
         const uint8_t* src = surv + b0 * in_b;
         if (!pinned) {
-          par_memcpy(h, src, cnt * in_b);
+          par_memcpy(c, h, src, cnt * in_b);
           src = h;
         }
         return hip_rc(hipMemcpyAsync(d, src, cnt * in_b, hipMemcpyHostToDevice, st));
@@ -1027,7 +1338,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
         return MEMO_EC_OK;
       },
       [&](int s, size_t b0, size_t cnt) {
-        if (!pinned) par_memcpy(out + b0 * out_b, c->h_slot[s] + o_out, cnt * out_b);
+        if (!pinned) par_memcpy(c, out + b0 * out_b, c->h_slot[s] + o_out, cnt * out_b);
       });
   if (rc) return rc;
   const uint32_t st = *c->h_status;
@@ -1057,7 +1368,7 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
     if (segs[i].m == 0 || segs[i].n == 0) continue;
     if (segs[i].S == 0 || segs[i].S % 64 || !segs[i].data || !segs[i].parity)
       return MEMO_EC_EINVAL;
-    if (segs[i].n > max_blocks_per_launch(segs[i].S)) return MEMO_EC_ERANGE;
+    if (segs[i].n > max_blocks_per_launch(c, segs[i].S)) return MEMO_EC_ERANGE;
     const int kc = mac_kchunk(segs[i].k, mac_rbound(segs[i].m));
     size_t ci = 0;
     while (ci < classes.size() && classes[ci] != kc) ++ci;
@@ -1084,8 +1395,201 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
     if (lds_of(launches[ci]) > 160 * 1024) return MEMO_EC_ERANGE;
   }
   for (auto& plans : launches)
-    if (int rc = launch_plans(plans, c->stream)) return rc;
+    if (int rc = launch_plans(c, plans, c->stream)) return rc;
   return MEMO_EC_OK;
+}
+
+int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segment* segs, int where) {
+  if (!c || nseg < 0 || nseg > MEMO_EC_MAX_REBUILD_SEGMENTS || (nseg && !segs)) return MEMO_EC_EINVAL;
+  if (where != MEMO_EC_DEVICE && where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED)
+    return MEMO_EC_EINVAL;
+  DeviceGuard g(c->device);
+  std::vector<RPiece> ps;
+  if (int rc = plan_rebuild_segments(c, nseg, segs, ps)) return rc;
+  if (ps.empty()) return MEMO_EC_OK;
+  if (where == MEMO_EC_DEVICE) {
+    if (int rc = ensure_tabs(c, rows_bytes(ps))) return rc;
+    if (int rc = launch_rebuild_pieces(c, ps, reinterpret_cast<uint8_t*>(c->d_tabs), c->stream,
+                                       c->d_status + kStatusDevice))
+      return rc;
+    // marks the scratch busy until these rebuilds are done (host calls check it)
+    return hip_rc(hipEventRecord(c->ev_order, c->stream));
+  }
+  const bool pinned = where == MEMO_EC_HOST_PINNED;
+  // device rebuilds still pending on the ctx stream read the same scratch
+  const hipError_t q = hipEventQuery(c->ev_order);
+  if (q == hipErrorNotReady) {
+    HIPCHK(hipStreamWaitEvent(c->sk, c->ev_order, 0));
+  } else if (q != hipSuccess) {
+    return hip_rc(q);
+  }
+  // Chunks of at most one pipeline batch of survivors, packed in order into
+  // waves of at most one batch; a wave's slot holds [survivors | outputs |
+  // per-block indices].
+  struct Chunk {
+    RPiece p;  // host pointers
+    size_t in, out, idx;
+    size_t o_in = 0, o_out = 0, o_idx = 0;
+  };
+  std::vector<Chunk> ch;
+  const size_t pipe = c->opt.pipe_bytes;
+  size_t total = 0;
+  for (const RPiece& p : ps) {
+    const size_t in_b = (size_t)p.k * p.S, out_b = (size_t)p.e * p.S;
+    const bool uni = p.mode == MAC_ENCODE;
+    const size_t per = std::max<size_t>(1, pipe / in_b);
+    for (size_t b0 = 0; b0 < p.n; b0 += per) {
+      Chunk x;
+      x.p = p;
+      x.p.b0 = b0;
+      x.p.n = std::min(per, p.n - b0);
+      x.p.surv = p.surv + b0 * in_b;
+      x.p.out = p.out + b0 * out_b;
+      if (!uni) {
+        x.p.sidx = p.sidx + b0 * (size_t)p.k;
+        x.p.lidx = p.lidx + b0 * (size_t)p.e;
+      }
+      x.in = x.p.n * in_b;
+      x.out = x.p.n * out_b;
+      x.idx = uni ? 0 : x.p.n * (size_t)(p.k + p.e);
+      total += x.in + x.out + x.idx;
+      ch.push_back(x);
+    }
+  }
+  struct Wave {
+    std::vector<size_t> ids;
+    size_t in = 0, out = 0, idx = 0, rows = 0;
+  };
+  std::vector<Wave> waves;
+  const bool zc = total + 64 <= zc_max_bytes(c);
+  for (size_t i = 0; i < ch.size(); ++i) {
+    if (waves.empty() || (!zc && waves.back().in + ch[i].in > pipe)) waves.emplace_back();
+    Wave& w = waves.back();
+    w.ids.push_back(i);
+    w.in += ch[i].in;
+    w.out += ch[i].out;
+    w.idx += ch[i].idx;
+    if (ch[i].p.mode == MAC_ROWS) w.rows += ch[i].p.n * (size_t)ch[i].p.e * ch[i].p.k;
+  }
+  size_t slot = 0, rows = 0;
+  for (Wave& w : waves) {
+    size_t oi = 0, oo = w.in, ox = w.in + w.out;
+    for (size_t i : w.ids) {
+      ch[i].o_in = oi;
+      ch[i].o_out = oo;
+      ch[i].o_idx = ox;
+      oi += ch[i].in;
+      oo += ch[i].out;
+      ox += ch[i].idx;
+    }
+    slot = std::max(slot, w.in + w.out + w.idx);
+    rows = std::max(rows, w.rows);
+  }
+  rows = (rows + 255) & ~(size_t)255;
+  // the pieces as the kernels see them, in slot memory at base (surv / out
+  // at the caller's pinned buffers when pinned_io)
+  auto staged = [&](const Wave& w, uint8_t* base, bool pinned_io) {
+    std::vector<RPiece> dp;
+    for (size_t i : w.ids) {
+      RPiece p = ch[i].p;
+      if (!pinned_io) {
+        p.surv = base + ch[i].o_in;
+        p.out = base + ch[i].o_out;
+      }
+      if (p.mode != MAC_ENCODE) {
+        p.sidx = base + ch[i].o_idx;
+        p.lidx = base + ch[i].o_idx + p.n * (size_t)p.k;
+      }
+      dp.push_back(p);
+    }
+    return dp;
+  };
+  auto stage_idx = [&](const Wave& w, uint8_t* h) {
+    for (size_t i : w.ids) {
+      const RPiece& p = ch[i].p;
+      if (p.mode == MAC_ENCODE) continue;
+      std::memcpy(h + ch[i].o_idx, p.sidx, p.n * (size_t)p.k);
+      std::memcpy(h + ch[i].o_idx + p.n * (size_t)p.k, p.lidx, p.n * (size_t)p.e);
+    }
+  };
+  if (zc) {
+    // Small call: the kernels read the survivors and indices from, and
+    // write their output to, pinned host memory (no DMA copies); the status
+    // word rides in the slot.
+    const Wave& w = waves[0];
+    if (int rc = ensure_slots(c, 0, slot + 64)) return rc;
+    if (int rc = ensure_tabs(c, rows)) return rc;
+    uint8_t* h = c->h_slot[0];
+    uint32_t* h_st = reinterpret_cast<uint32_t*>(h + ((slot + 3) & ~(size_t)3));
+    *h_st = 0;
+    stage_idx(w, h);
+    if (!pinned)
+      for (size_t i : w.ids) par_memcpy(c, h + ch[i].o_in, ch[i].p.surv, ch[i].in);
+    if (int rc = launch_rebuild_pieces(c, staged(w, h, pinned), reinterpret_cast<uint8_t*>(c->d_tabs),
+                                       c->sk, h_st))
+      return rc;
+    HIPCHK(hipStreamSynchronize(c->sk));
+    if (!pinned)
+      for (size_t i : w.ids) par_memcpy(c, ch[i].p.out, h + ch[i].o_out, ch[i].out);
+    int drc = c->deferred;
+    c->deferred = 0;
+    if (drc == MEMO_EC_OK && (__atomic_load_n(h_st, __ATOMIC_ACQUIRE) & 1u)) drc = MEMO_EC_ESINGULAR;
+    return drc;
+  }
+  if (int rc = ensure_slots(c, slot, slot)) return rc;
+  if (int rc = ensure_tabs(c, kSlots * rows)) return rc;
+  const int rc = run_waves(
+      c, waves.size(),
+      [&](int s, size_t wi, hipStream_t st) -> int {
+        const Wave& w = waves[wi];
+        uint8_t* h = c->h_slot[s];
+        uint8_t* d = c->d_slot[s];
+        stage_idx(w, h);
+        if (w.idx) HIPCHK(hipMemcpyAsync(d + w.in + w.out, h + w.in + w.out, w.idx, hipMemcpyHostToDevice, st));
+        for (size_t i : w.ids) {
+          if (pinned) {
+            HIPCHK(hipMemcpyAsync(d + ch[i].o_in, ch[i].p.surv, ch[i].in, hipMemcpyHostToDevice, st));
+          } else {
+            par_memcpy(c, h + ch[i].o_in, ch[i].p.surv, ch[i].in);
+          }
+        }
+        if (!pinned) HIPCHK(hipMemcpyAsync(d, h, w.in, hipMemcpyHostToDevice, st));
+        return MEMO_EC_OK;
+      },
+      [&](int s, size_t wi, hipStream_t st) -> int {
+        return launch_rebuild_pieces(c, staged(waves[wi], c->d_slot[s], false),
+                                     reinterpret_cast<uint8_t*>(c->d_tabs) + (size_t)s * rows, st,
+                                     c->d_status + kStatusPipeline);
+      },
+      [&](int s, size_t wi, hipStream_t st) -> int {
+        const Wave& w = waves[wi];
+        uint8_t* d = c->d_slot[s];
+        if (pinned) {
+          for (size_t i : w.ids)
+            HIPCHK(hipMemcpyAsync(ch[i].p.out, d + ch[i].o_out, ch[i].out, hipMemcpyDeviceToHost, st));
+        } else {
+          HIPCHK(hipMemcpyAsync(c->h_slot[s] + w.in, d + w.in, w.out, hipMemcpyDeviceToHost, st));
+        }
+        // the deferred-error word rides behind the last wave's output
+        if (wi + 1 == waves.size())
+          HIPCHK(hipMemcpyAsync(c->h_status, c->d_status + kStatusPipeline, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, st));
+        return MEMO_EC_OK;
+      },
+      [&](int s, size_t wi) {
+        if (pinned) return;
+        for (size_t i : waves[wi].ids) par_memcpy(c, ch[i].p.out, c->h_slot[s] + ch[i].o_out, ch[i].out);
+      });
+  if (rc) return rc;
+  const uint32_t st = *c->h_status;
+  if (st) {
+    HIPCHK(hipMemsetAsync(c->d_status + kStatusPipeline, 0, sizeof(uint32_t), c->sd));
+    HIPCHK(hipStreamSynchronize(c->sd));
+  }
+  int drc = c->deferred;
+  c->deferred = 0;
+  if (drc == MEMO_EC_OK && (st & 1u)) drc = MEMO_EC_ESINGULAR;
+  return drc;
 }
 
 int memo_ec_sha256_batch(memo_ec_ctx* c, size_t n, const uint8_t* prefix, size_t prefix_len,

@@ -43,6 +43,28 @@ class Segment(ctypes.Structure):
                 ("data", ctypes.c_void_p), ("parity", ctypes.c_void_p)]
 
 
+class RebuildSegment(ctypes.Structure):
+    """memo_ec_rebuild_segment (include/memo_ec.h)."""
+    _fields_ = [("k", ctypes.c_int), ("m", ctypes.c_int), ("S", _sz), ("n", _sz),
+                ("surv_idx", ctypes.c_void_p), ("surv", ctypes.c_void_p),
+                ("lost_idx", ctypes.c_void_p), ("e", ctypes.c_int), ("uniform", ctypes.c_int),
+                ("out", ctypes.c_void_p)]
+
+
+# memo_ec_option (include/memo_ec.h)
+OPTIONS = {"rebuild_path": 1, "fused_max_bytes": 2, "zero_copy_bytes": 3, "pipe_bytes": 4,
+           "copy_threads": 5, "max_launch_tiles": 6, "xcd_min_tiles": 7, "decode_wide_max": 8,
+           "decode_exact": 9, "decode_stage": 10}
+MAX_REBUILD_SEGMENTS = 256
+
+# The sources memo_ec_build_id() hashes, in its order (memo_amd/csrc/Makefile).
+_ROOT = os.path.dirname(_HERE)
+BUILD_SOURCES = [os.path.join(_ROOT, "include", "memo_ec.h"),
+                 os.path.join(_HERE, "csrc", "ec_kernels.h"),
+                 os.path.join(_HERE, "csrc", "ec_kernels.hip"),
+                 os.path.join(_HERE, "csrc", "memo_ec.cpp")]
+
+
 _LIB = None
 
 EXPORTS = [
@@ -52,7 +74,8 @@ EXPORTS = [
     "memo_ec_host_alloc", "memo_ec_host_free", "memo_ec_encode_segments",
     "memo_ec_sha256_batch", "memo_ec_fill_blocks", "memo_ec_erasures", "memo_ec_gather_shards",
     "memo_ec_strerror",
-    "memo_ec_version", "memo_ec_device_count",
+    "memo_ec_version", "memo_ec_device_count", "memo_ec_rebuild_segments",
+    "memo_ec_ctx_set_option", "memo_ec_ctx_get_option", "memo_ec_build_id",
 ]
 
 
@@ -92,6 +115,11 @@ def _lib():
         L.memo_ec_strerror.restype = ctypes.c_char_p
         L.memo_ec_version.restype = c_int
         L.memo_ec_device_count.restype = c_int
+        L.memo_ec_rebuild_segments.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(RebuildSegment),
+                                               c_int]
+        L.memo_ec_ctx_set_option.argtypes = [ctypes.c_void_p, c_int, ctypes.c_int64]
+        L.memo_ec_ctx_get_option.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(ctypes.c_int64)]
+        L.memo_ec_build_id.restype = ctypes.c_char_p
         _LIB = L
     return _LIB
 
@@ -99,6 +127,30 @@ def _lib():
 def _check(rc, what=""):
     if rc != 0:
         raise MemoECError(rc, what)
+
+
+def build_id():
+    """SHA-256 of the sources the loaded library was built from."""
+    return _lib().memo_ec_build_id().decode()
+
+
+def source_id():
+    """SHA-256 of the library's sources in this tree (what build_id() must be)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in BUILD_SOURCES:
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def check_build():
+    """Raise unless the loaded library was built from this tree's sources."""
+    b, s = build_id(), source_id()
+    if b != s:
+        raise RuntimeError("libmemo_ec.so build id %s does not match the sources (%s): rebuild "
+                           "with __graft_entry__.build()" % (b[:16], s[:16]))
+    return b
 
 
 def shard_size(block_bytes, k):
@@ -217,6 +269,31 @@ class Codec:
     def synchronize(self):
         _check(_lib().memo_ec_synchronize(self._ctx), "synchronize")
 
+    # -- tuning (memo_ec_ctx_set_option)
+    def set_option(self, name, value):
+        _check(_lib().memo_ec_ctx_set_option(self._ctx, OPTIONS[name], int(value)), "set_option")
+
+    def get_option(self, name):
+        v = ctypes.c_int64()
+        _check(_lib().memo_ec_ctx_get_option(self._ctx, OPTIONS[name], ctypes.byref(v)), "get_option")
+        return v.value
+
+    def options(self, **kw):
+        """Context manager: set options for a block of calls, then restore them."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_option(k) for k in kw}
+            try:
+                for k, v in kw.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+        return cm()
+
     # -- codec
     def encode(self, k, m, data, parity, S=None, n=None):
         """parity (n x m x S) <- data (n x k x S); device (async) or host (sync)."""
@@ -272,6 +349,41 @@ class Codec:
         _check(_lib().memo_ec_decode_rows(self._ctx, k, m, n, _ptr(surv_idx)[0], _ptr(lost_idx)[0],
                                           e, _ptr(rows)[0]), "decode_rows")
         return rows
+
+    def rebuild_segments(self, segs):
+        """One memo_ec_rebuild_segments call.  segs: list of dicts with k, m,
+        surv_idx, surv, lost_idx, out and optionally uniform (then surv_idx /
+        lost_idx are host sequences of k / e indices).  Buffers: all device
+        tensors (asynchronous) or all host (numpy / pinned torch; synchronous)."""
+        arr = (RebuildSegment * len(segs))()
+        keep, wheres = [], set()
+        for i, s in enumerate(segs):
+            k, m = s["k"], s["m"]
+            sp, sw = _ptr(s["surv"])
+            op, ow = _ptr(s["out"])
+            n, S = (s["n"], s["S"]) if "S" in s else _infer_nS(s["surv"], k)
+            uni = bool(s.get("uniform", False))
+            if uni:
+                si = np.ascontiguousarray(np.asarray(s["surv_idx"], dtype=np.uint8).reshape(-1))
+                li = np.ascontiguousarray(np.asarray(s["lost_idx"], dtype=np.uint8).reshape(-1))
+                keep += [si, li]
+                ip, lp, e = si.ctypes.data, li.ctypes.data, len(li)
+            else:
+                ip, iw = _ptr(s["surv_idx"])
+                lp, lw = _ptr(s["lost_idx"])
+                e = s["lost_idx"].shape[1]
+                wheres.update({iw if iw == DEVICE else HOST, lw if lw == DEVICE else HOST})
+            wheres.update({sw if sw == DEVICE else HOST, ow if ow == DEVICE else HOST})
+            arr[i] = RebuildSegment(k, m, S, n, ip, sp, lp, e, int(uni), op)
+        if len(wheres) > 1:
+            raise ValueError("rebuild_segments: mix of device and host buffers")
+        if DEVICE in wheres:
+            where = DEVICE
+        else:
+            allp = all(_ptr(s["surv"])[1] == HOST_PINNED and _ptr(s["out"])[1] == HOST_PINNED
+                       for s in segs)
+            where = HOST_PINNED if allp else HOST
+        _check(_lib().memo_ec_rebuild_segments(self._ctx, len(segs), arr, where), "rebuild_segments")
 
     def encode_segments(self, segs):
         """segs: list of (k, m, S, n, data_tensor, parity_tensor) on this device."""

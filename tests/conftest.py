@@ -34,6 +34,7 @@ def codec():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from memo_amd import ec
+    ec.check_build()  # the loaded kernels were built from this tree's sources
     c = ec.Codec(0)
     yield c
     c.close()
@@ -43,6 +44,13 @@ def codec():
 def rebuild_path(request, monkeypatch):
     """Run a rebuild test on both device rebuild paths: the fused
     gf_rebuild_kernel (default) and the two-kernel decode_coef_kernel +
-    gf_mac_kernel path (MEMO_EC_REBUILD_FUSED=0, read per call)."""
-    monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", "1" if request.param == "fused" else "0")
-    return request.param
+    gf_mac_kernel path: the session codec's MEMO_EC_OPT_REBUILD_PATH, and
+    MEMO_EC_REBUILD_FUSED for contexts the test creates itself."""
+    v = 1 if request.param == "fused" else 0
+    monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", str(v))
+    if "codec" in request.fixturenames:
+        c = request.getfixturevalue("codec")
+        with c.options(rebuild_path=v):
+            yield request.param
+    else:
+        yield request.param

@@ -50,14 +50,23 @@ def test_host_functions_match_oracle(O):
 def test_error_codes_and_limits():
     from memo_amd import ec
     L = ec._lib()
-    assert L.memo_ec_version() == 1
+    assert L.memo_ec_version() == 2
     assert L.memo_ec_strerror(-4) == b"survivor shards cannot rebuild the block"
     with pytest.raises(ec.MemoECError):
         ec.generator(65, 4)
     with pytest.raises(ec.MemoECError):
         ec.generator(0, 4)
-    c = ctypes.c_void_p()
     assert L.memo_ec_encode_batch(None, 10, 4, 64, 1, None, None, 2) == -1
+    assert L.memo_ec_rebuild_segments(None, 0, None, 2) == -1
+    assert L.memo_ec_ctx_set_option(None, 1, 0) == -1
+
+
+def test_build_id_matches_sources():
+    """The library in the tree was built from the sources in the tree
+    (memo_ec_build_id() == SHA-256 of include/memo_ec.h + the csrc files)."""
+    from memo_amd import ec
+    assert len(ec.build_id()) == 64
+    assert ec.check_build() == ec.source_id()
 
 
 def test_no_gpu_fails_loudly():

@@ -135,13 +135,18 @@ def test_random_geometries_vs_oracle(codec, O, seed, rebuild_path):
         assert np.array_equal(host(ou), O.gather(k, m, S, data, want, lu)), case + (e, "uniform")
 
 
-def test_batches_split_across_launches(codec, O, monkeypatch, rebuild_path):
+@pytest.fixture
+def split_launches(codec):
+    with codec.options(max_launch_tiles=600):  # 22 1-MiB RS(10,4) blocks per launch
+        yield
+
+
+def test_batches_split_across_launches(codec, O, split_launches, rebuild_path):
     """A batch larger than one launch's grid is split into several MAC
     launches (memo_ec.cpp max_blocks_per_launch); the bound is lowered so the
     split happens at a testable size.  Encode and rebuild, device and host."""
     k, m, B, n = 10, 4, 1 << 20, 64
     S = O.shard_size(B, k)
-    monkeypatch.setenv("MEMO_EC_MAX_LAUNCH_TILES", "600")  # 22 blocks per launch
     data = O.fill_blocks(SEED, 9, n, B, k, S)
     want = O.encode(k, m, S, data, threads=4)
     p = empty(n, m * S)
@@ -215,23 +220,26 @@ def test_every_erasure_pattern_in_one_batch(codec, O, k, m, rebuild_path):
 @pytest.mark.parametrize("k,m", [(1, 1), (2, 2), (3, 2), (4, 2), (6, 3), (7, 5), (8, 8), (10, 4),
                                  (12, 4), (14, 2), (16, 4), (16, 16), (20, 8), (33, 12), (64, 16)])
 @pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_staged", "per_block_generic"])
-def test_decode_rows_vs_oracle(codec, O, k, m, kernel, monkeypatch):
+def test_decode_rows_vs_oracle(codec, O, k, m, kernel):
     """Closed-form decode rows against the oracle's Gauss-Jordan rows
     C[lost] * inv(C[surv]): random survivor orders, lost shards that are
     data, parity or themselves survivors (unit rows), e = 1..m, over 700
     blocks (several workgroups).  Both kernels: column-per-lane
     (decode_coef_wide_kernel, small batches) and one lane per block
-    (forced by MEMO_EC_DECODE_WIDE_MAX=0: decode_rows_k_kernel for k in
+    (forced by decode_wide_max=0: decode_rows_k_kernel for k in
     {2, 3, 4, 6, 8, 10, 12, 14, 16}, decode_coef_kernel otherwise or with
-    MEMO_EC_DECODE_EXACT=0).  The exact-k kernel stores whole-dword rows
-    from registers, other rows through LDS (all of them with
-    MEMO_EC_DECODE_STAGE=1)."""
-    if kernel != "wide":
-        monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
-    if kernel == "per_block_generic":
-        monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
-    if kernel == "per_block_staged":
-        monkeypatch.setenv("MEMO_EC_DECODE_STAGE", "1")
+    decode_exact=0).  The exact-k kernel stores whole-dword rows from
+    registers, other rows through LDS (all of them with decode_stage=1)."""
+    with codec.options(**DECODE_KERNELS[kernel]):
+        _decode_rows_vs_oracle(codec, O, k, m)
+
+
+DECODE_KERNELS = {"wide": {}, "per_block": {"decode_wide_max": 0},
+                  "per_block_staged": {"decode_wide_max": 0, "decode_stage": 1},
+                  "per_block_generic": {"decode_wide_max": 0, "decode_exact": 0}}
+
+
+def _decode_rows_vs_oracle(codec, O, k, m):
     rng = np.random.default_rng(k * 1000 + m)
     n = 700
     for e in sorted({1, (m + 1) // 2, m}):
@@ -344,13 +352,17 @@ def test_host_memory_paths(codec, O):
     assert np.array_equal(out, O.gather(k, m, S, data, want, l))
 
 
-@pytest.mark.parametrize("zc_kb", ["256", "0"])
-def test_small_host_calls(codec, O, zc_kb, monkeypatch):
+@pytest.mark.parametrize("zc_kb", [256, 0])
+def test_small_host_calls(codec, O, zc_kb):
     """One-block and few-block calls from pageable and pinned host memory,
-    with the zero-copy path (kernels on pinned host memory, MEMO_EC_ZC_KB
-    default) and without it (DMA copies)."""
+    with the zero-copy path (kernels on pinned host memory) and without it
+    (DMA copies)."""
+    with codec.options(zero_copy_bytes=zc_kb << 10):
+        _small_host_calls(codec, O)
+
+
+def _small_host_calls(codec, O):
     import torch
-    monkeypatch.setenv("MEMO_EC_ZC_KB", zc_kb)
     k, m = 10, 4
     for B, n in ((4096, 1), (100000, 3), (4096, 7)):
         S = O.shard_size(B, k)
@@ -385,16 +397,15 @@ def test_singular_survivors_reported(codec, rebuild_path):
 
 
 @pytest.mark.parametrize("kernel", ["wide", "per_block", "per_block_staged", "per_block_generic"])
-def test_invalid_sets_give_zero_rows(codec, O, kernel, monkeypatch):
+def test_invalid_sets_give_zero_rows(codec, O, kernel):
     """Duplicate survivors, a survivor index >= k+m and a lost index >= k+m
     zero that block's rows (only that block's) and raise ESINGULAR once."""
+    with codec.options(**DECODE_KERNELS[kernel]):
+        _invalid_sets_give_zero_rows(codec, O)
+
+
+def _invalid_sets_give_zero_rows(codec, O):
     from memo_amd import ec
-    if kernel != "wide":
-        monkeypatch.setenv("MEMO_EC_DECODE_WIDE_MAX", "0")
-    if kernel == "per_block_generic":
-        monkeypatch.setenv("MEMO_EC_DECODE_EXACT", "0")
-    if kernel == "per_block_staged":
-        monkeypatch.setenv("MEMO_EC_DECODE_STAGE", "1")
     k, m, e = 10, 4, 2
     surv = np.array([list(range(10)), [0, 1, 2, 3, 4, 5, 6, 7, 8, 8], [0, 1, 2, 3, 4, 5, 6, 7, 8, 14],
                      [13, 1, 2, 3, 4, 5, 6, 7, 8, 9], list(range(10))], np.uint8)

@@ -1,0 +1,171 @@
+"""GPU parity of the mixed-geometry rebuild (memo_ec_rebuild_segments): one
+call over groups with different (k, m), block sizes, erasure counts and
+per-block or shared erasure patterns -- the read side of the reference's
+multi-address fetch, which hands a whole batch over at once
+(src/memo/model/doughnut/Consensus.cc:101-124, consensus/Paxos.cc:1857-1890).
+Every rebuilt shard is compared with the CPU oracle's shards, bit-exact."""
+import numpy as np
+import pytest
+
+from conftest import SEED
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+def empty(*shape):
+    import torch
+    return torch.empty(shape, dtype=torch.uint8, device="cuda")
+
+
+def make_groups(O, spec, seed):
+    """spec: (k, m, B, n, e, uniform) per group -> host-side cases with the
+    survivors, patterns and the oracle's lost shards."""
+    rng = np.random.default_rng(seed)
+    groups = []
+    for gi, (k, m, B, n, e, uni) in enumerate(spec):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 1000 * gi + seed, n, B, k, S)
+        par = O.encode(k, m, S, data, threads=4)
+        if uni:
+            perm = rng.permutation(k + m)
+            su, lu = perm[:k].astype(np.uint8), perm[k:k + e].astype(np.uint8)
+            s, l = np.tile(su, (n, 1)), np.tile(lu, (n, 1))
+        else:
+            # random survivor orders; lost shards that are data or parity
+            s = np.stack([rng.permutation(k + m)[:k] for _ in range(n)]).astype(np.uint8)
+            l = np.stack([np.setdiff1d(np.arange(k + m), x)[rng.permutation(m)[:e]] for x in s]).astype(np.uint8)
+            su = lu = None
+        groups.append(dict(k=k, m=m, S=S, n=n, e=e, uniform=uni, s=s, l=l, su=su, lu=lu,
+                           surv=O.gather(k, m, S, data, par, s), want=O.gather(k, m, S, data, par, l)))
+    return groups
+
+
+C5_MIX = [(k, m, B, n, e, uni)
+          for (k, m) in [(4, 2), (10, 4), (16, 4)]
+          for (B, n) in [(4096, 60), (65536, 9), (1 << 20, 3), (4 << 20, 1)]
+          for (e, uni) in [(m, False)]] + [
+    (10, 4, 4096, 40, 1, False), (16, 4, 65536, 5, 2, False), (4, 2, 4096, 33, 1, True),
+    (10, 4, 65536, 7, 4, True), (16, 4, 1 << 20, 2, 3, True)]
+
+
+def device_segs(groups):
+    segs = []
+    for g in groups:
+        d = dict(k=g["k"], m=g["m"], surv=dev(g["surv"]), out=empty(g["n"], g["e"] * g["S"]),
+                 uniform=g["uniform"])
+        if g["uniform"]:
+            d.update(surv_idx=g["su"], lost_idx=g["lu"])
+        else:
+            d.update(surv_idx=dev(g["s"]), lost_idx=dev(g["l"]))
+        segs.append(d)
+    return segs
+
+
+def test_mixed_c5_rebuild_one_call_vs_oracle(codec, O, rebuild_path):
+    """(4,2)/(10,4)/(16,4) x 4 KiB/64 KiB/1 MiB/4 MiB with e = m random
+    per-block patterns, plus per-block groups with e < m and shared-pattern
+    groups, device-resident, in ONE call."""
+    groups = make_groups(O, C5_MIX, 1)
+    segs = device_segs(groups)
+    codec.rebuild_segments(segs)
+    codec.synchronize()
+    for g, s in zip(groups, segs):
+        assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (g["k"], g["m"], g["S"], g["e"])
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("mode", ["zero_copy", "one_wave", "many_waves"])
+def test_mixed_rebuild_host_memory(codec, O, pinned, mode, rebuild_path):
+    """The same mixed call from host memory (pageable numpy or pinned torch
+    buffers): the zero-copy path, one pipeline wave, and waves cut by a
+    1 MiB pipeline batch (segments split across waves)."""
+    import torch
+    spec = C5_MIX if mode != "zero_copy" else [(4, 2, 4096, 5, 2, False), (10, 4, 4096, 3, 4, False),
+                                                (16, 4, 8192, 2, 1, True), (10, 4, 65536, 1, 3, False)]
+    groups = make_groups(O, spec, 2)
+    opts = {"zero_copy": dict(zero_copy_bytes=4 << 20), "one_wave": dict(zero_copy_bytes=0),
+            "many_waves": dict(zero_copy_bytes=0, pipe_bytes=1 << 20)}[mode]
+    segs = []
+    for g in groups:
+        surv = torch.from_numpy(g["surv"]).pin_memory() if pinned else g["surv"]
+        out = (torch.zeros((g["n"], g["e"] * g["S"]), dtype=torch.uint8).pin_memory() if pinned
+               else np.zeros((g["n"], g["e"] * g["S"]), np.uint8))
+        d = dict(k=g["k"], m=g["m"], surv=surv, out=out, uniform=g["uniform"])
+        d.update(surv_idx=g["su"], lost_idx=g["lu"]) if g["uniform"] else d.update(surv_idx=g["s"],
+                                                                                    lost_idx=g["l"])
+        segs.append(d)
+    with codec.options(**opts):
+        codec.rebuild_segments(segs)
+    for g, s in zip(groups, segs):
+        assert np.array_equal(np.asarray(s["out"]), g["want"]), (mode, g["k"], g["S"], g["e"])
+
+
+def test_many_segments_and_patterns(codec, O, rebuild_path):
+    """More segments than one launch holds (12) in one class, and more shared
+    patterns than the ctx's pattern cache (64) in one call: every table the
+    call formed stays alive until its launch."""
+    spec = [(10, 4, 4096, 3, 1 + i % 4, i % 3 == 0) for i in range(90)] + \
+           [(16, 4, 4096, 2, 2, True) for _ in range(40)]
+    groups = make_groups(O, spec, 3)
+    segs = device_segs(groups)
+    codec.rebuild_segments(segs)
+    codec.synchronize()
+    for i, (g, s) in enumerate(zip(groups, segs)):
+        assert np.array_equal(s["out"].cpu().numpy(), g["want"]), i
+
+
+def test_segments_split_across_launches(codec, O, rebuild_path):
+    """A segment longer than one launch's grid is split by blocks."""
+    groups = make_groups(O, [(10, 4, 1 << 20, 30, 4, False), (10, 4, 1 << 20, 25, 2, True),
+                             (4, 2, 1 << 20, 9, 2, False)], 4)
+    segs = device_segs(groups)
+    with codec.options(max_launch_tiles=600):
+        codec.rebuild_segments(segs)
+    codec.synchronize()
+    for g, s in zip(groups, segs):
+        assert np.array_equal(s["out"].cpu().numpy(), g["want"])
+
+
+def test_segments_bad_patterns(codec, O, rebuild_path):
+    """A bad per-block survivor set zeroes only that block and raises
+    ESINGULAR (device: at synchronize; host: from the call), the other
+    blocks and segments are rebuilt; a bad shared pattern is refused before
+    anything is enqueued; empty segments (n = 0 or e = 0) are no-ops."""
+    from memo_amd import ec
+    groups = make_groups(O, [(10, 4, 4096, 6, 2, False), (4, 2, 65536, 3, 2, False)], 5)
+    bad = groups[0]["s"].copy()
+    bad[2, 1] = bad[2, 0]
+    segs = device_segs(groups)
+    segs[0]["surv_idx"] = dev(bad)
+    codec.rebuild_segments(segs)
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.synchronize()
+    assert ei.value.code == -4
+    got = segs[0]["out"].cpu().numpy()
+    good = np.ones(6, bool)
+    good[2] = False
+    assert not got[2].any()
+    assert np.array_equal(got[good], groups[0]["want"][good])
+    assert np.array_equal(segs[1]["out"].cpu().numpy(), groups[1]["want"])
+    codec.synchronize()
+    # host memory: the error comes back from the call itself
+    hs = [dict(k=10, m=4, surv=groups[0]["surv"], surv_idx=bad, lost_idx=groups[0]["l"],
+               out=np.zeros_like(groups[0]["want"]))]
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.rebuild_segments(hs)
+    assert ei.value.code == -4
+    assert np.array_equal(hs[0]["out"][good], groups[0]["want"][good])
+    # a shared pattern with a duplicate survivor: refused up front
+    o = empty(2, 4096)
+    with pytest.raises(ec.MemoECError) as ei:
+        codec.rebuild_segments([dict(k=10, m=4, surv=empty(2, 10 * 4096), out=o, uniform=True,
+                                     surv_idx=[0, 1, 2, 3, 4, 5, 6, 7, 8, 8], lost_idx=[9])])
+    assert ei.value.code == -4
+    codec.rebuild_segments([dict(k=10, m=4, surv=empty(0, 640), out=empty(0, 64), n=0, S=64,
+                                 surv_idx=empty(0, 10), lost_idx=empty(0, 1))])
+    codec.synchronize()

@@ -133,6 +133,34 @@ def test_bench_assemble_per_rank_fields():
     for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                 "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
         assert key in res
+    # every rank's side measurements: rank 0's copy rate and PCIe rate, the
+    # node's per-rank list and sum
+    e2e = lambda p, q: {"pinned": {"value": p, "bit_exact": True}, "pageable": {"value": q, "bit_exact": True}}
+    extras = [{"copy_GBs": 5000.0, "e2e": e2e(48.0, 45.0), "lat": {"encode_4096B_us": 20.0}},
+              {"copy_GBs": 5100.0, "e2e": e2e(47.0, 44.0), "lat": {"encode_4096B_us": 21.0}}]
+    bench.merge_extras(res, extras)
+    assert res["roofline"]["copy_GBs"] == 5000.0
+    assert res["end_to_end"]["pinned"]["value"] == 48.0
+    assert res["end_to_end"]["node_sum"] == {"pinned": 95.0, "pageable": 89.0}
+    assert [x["rank"] for x in res["end_to_end"]["per_rank"]] == [0, 1]
+    assert res["host_call_latency"]["encode_4096B_us"] == 20.0
+
+
+def test_cpu_share_is_bounded():
+    """The CPU baseline's threads: the affinity set capped by the cgroup quota
+    and OMP_NUM_THREADS, at most 16."""
+    import bench
+    assert 1 <= bench.cpu_share() <= bench.host_cores()
+    assert 1 <= bench.cpu_threads() <= 16
+    old = os.environ.get("OMP_NUM_THREADS")
+    try:
+        os.environ["OMP_NUM_THREADS"] = "3"
+        assert bench.cpu_share() <= 3
+    finally:
+        if old is None:
+            os.environ.pop("OMP_NUM_THREADS")
+        else:
+            os.environ["OMP_NUM_THREADS"] = old
 
 
 def _bench_json(r):
@@ -144,7 +172,7 @@ def _bench_json(r):
 
 
 BENCH_SMALL = ["--gpus", "2", "--same-device", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
-               "--blocks", "64", "--no-cpu", "--no-e2e", "--no-small"]
+               "--blocks", "64", "--no-cpu", "--no-e2e", "--no-small", "--no-pmc"]
 
 
 @pytest.mark.gpu
@@ -178,3 +206,27 @@ def test_bench_two_ranks_under_torchrun():
     res = _bench_json(subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT))
     assert res["n_gpus"] == 2 and res["config"]["global_blocks"] == 128
     assert res["value"] > 0 and res["rebuild"]["round_trip_bit_exact"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_bench_n2_line_is_self_sufficient():
+    """At N = 2 the line still carries the CPU baseline (rank 0, after the
+    timed steps), every rank's PCIe end-to-end rate and their sum, the
+    counter-measured traffic of this run, and the loaded library's build id
+    (== the sources' hash)."""
+    import subprocess
+    import sys
+    args = ["--gpus", "2", "--same-device", "--steps", "3", "--warmup", "2", "--settle-ms", "0",
+            "--blocks", "256", "--no-small", "--cpu-seconds", "1"]
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args,
+                       capture_output=True, text=True, timeout=380, cwd=ROOT)
+    res = _bench_json(r)
+    assert res["n_gpus"] == 2
+    cb = res["cpu_baseline"]
+    assert cb["value"] > 0 and 1 <= cb["cores"] <= 16 and cb["bit_exact_vs_gpu"]
+    assert len(res["end_to_end"]["per_rank"]) == 2 and res["end_to_end"]["node_sum"]["pinned"] > 0
+    assert res["end_to_end"]["pinned"]["bit_exact"]
+    assert res["roofline"]["traffic"] > 0 and res["roofline"]["traffic_ratio"] < 1.5, res["roofline"]
+    assert res["roofline_rebuild"]["traffic"] > 0
+    assert res["build_matches_sources"]

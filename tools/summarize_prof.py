@@ -5,7 +5,7 @@ Writes
   profiles/<tag>_pmc.csv            per-dispatch FETCH_SIZE / WRITE_SIZE of the
                                     encode MAC and the rebuild MAC
   profiles/<tag>_summary.md         kernel times, algorithmic vs PMC bytes
-  profiles/pmc_traffic.json         per-launch HBM traffic read by bench.py
+(bench.py measures roofline.traffic itself, with its own counter passes.)
 
 The encode (gf_mac_kernel<KC, R, NT, false>) and the rebuild MAC
 (gf_mac_kernel<..., true>, after decode_coef*/decode_rows_k*) are told apart
@@ -66,8 +66,6 @@ def main():
             kd = kind(r["Kernel_Name"])
             if kd in alg:
                 pmc.setdefault((kd, what), []).append(float(r["Counter_Value"]))
-    tj = os.path.join(out_dir, "pmc_traffic.json")
-    t = json.load(open(tj)) if os.path.exists(tj) else {}
     with open(os.path.join(out_dir, "%s_pmc.csv" % tag), "w") as f:
         f.write("kernel,launch,FETCH_SIZE_KB,WRITE_SIZE_KB\n")
         for kd in alg:
@@ -107,10 +105,6 @@ def main():
         if fe and wr:
             f_med, w_med = statistics.median(fe), statistics.median(wr)
             hbm = (2 * f_med + w_med) * 1024
-            t[key] = {"hbm_bytes_per_launch": int(hbm), "algorithmic_bytes": alg[kd],
-                      "ratio": round(hbm / alg[kd], 4), "fetch_kb_median": f_med, "write_kb_median": w_med,
-                      "source": "profiles/%s_pmc.csv (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate "
-                                "passes; bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024)" % tag}
             md.append("PMC HBM bytes per %s launch: (2*%.0f + %.0f) KB * 1024 = %d (%.3f x the %d "
                       "algorithmic bytes)." % (kd, f_med, w_med, hbm, hbm / alg[kd], alg[kd]))
         md.append("")
@@ -118,7 +112,6 @@ def main():
         dd = durs["decode"][-steps:]
         md.append("Decode rows (4096 blocks, column-per-lane kernel): %.1f us per rebuild step." %
                   (statistics.mean(dd) * 1e3))
-    json.dump(t, open(tj, "w"), indent=1)
     open(os.path.join(out_dir, "%s_summary.md" % tag), "w").write("\n".join(md) + "\n")
     print("\n".join(md))
 
