@@ -112,13 +112,16 @@ int main(int argc, char** argv) {
   ec.fetch(addrs, check);
   const double t_degraded_cold = now() - t;
   bool degraded_ok = ok == nb;
-  const uint64_t dec0 = ec.codec().rebuild_calls();
+  auto codec_calls = [&] {
+    return ec.codec().rebuild_calls() + ec.codec().uniform_calls() + ec.codec().segments_calls();
+  };
+  const uint64_t dec0 = codec_calls();
   ok = 0;
   t = now();
   ec.fetch(addrs, check);
   const double t_degraded = now() - t;
   degraded_ok = degraded_ok && ok == nb;
-  const uint64_t degraded_calls = ec.codec().rebuild_calls() - dec0;
+  const uint64_t degraded_calls = codec_calls() - dec0;
 
   // they are evicted: rebuild their shards onto other nodes
   for (auto& n : en.nodes)

@@ -471,30 +471,36 @@ def test_noops_and_argument_errors(codec):
 
 
 def test_full_size_c2_c3_round_trip(codec, O, rebuild_path):
-    """BASELINE.json C2/C3 at full size (4096 x 1 MiB, RS(10,4), e=4):
-    sampled blocks bit-exact vs the oracle; every block's 4 erased shards
-    rebuilt bit-exact (device-side comparison)."""
+    """BASELINE.json C2/C3 at full size (4096 x 1 MiB, RS(10,4), e=4), the
+    WHOLE batch against the CPU oracle: all 4096 blocks' data and parity
+    (vectorised oracle encode, oracle/rs_simd.c, bit-exact with the scalar
+    oracle) and all 4096 x 4 rebuilt shards (the oracle's own per-block
+    decode rows + vectorised MAC); then data shards alone (lost = all
+    parity) re-encode identically."""
     import torch
     k, m, B, n, e = 10, 4, 1 << 20, 4096, 4
     S = O.shard_size(B, k)
     d = fill(codec, 0, n, B, k, S)
     p = empty(n, m * S)
     codec.encode(k, m, d, p)
-    codec.synchronize()
-    for b in [0, 1, 777, 2048, n - 1]:
-        data = O.fill_blocks(SEED, b, 1, B, k, S)
-        assert np.array_equal(host(p[b:b + 1]), O.encode(k, m, S, data)), b
     s, l = ec_erasures(n, k, m, e)
     sd, ld = dev(s), dev(l)
     surv = empty(n, k * S)
     codec.gather_shards(k, m, S, n, d, p, sd, surv)
     out = empty(n, e * S)
     codec.rebuild(k, m, sd, surv, ld, out)
-    want = empty(n, e * S)
-    codec.gather_shards(k, m, S, n, d, p, ld, want)
     codec.synchronize()
-    assert torch.equal(out, want)
-    del surv, want
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    assert np.array_equal(host(d), data)
+    par, _ = O.encode_simd(k, m, S, data, threads=16)
+    assert np.array_equal(host(p), par)
+    del surv
+    hs = O.gather(k, m, S, data, par, s)
+    want, _ = O.rebuild_simd(k, m, S, s, hs, l, threads=16)
+    del hs
+    assert np.array_equal(host(out), want)
+    assert np.array_equal(want, O.gather(k, m, S, data, par, l))
+    del want, out
     # data shards alone (lost = all parity) re-encode identically
     lp = dev(np.tile(np.arange(k, k + m, dtype=np.uint8), (n, 1)))
     sp = dev(np.tile(np.arange(k, dtype=np.uint8), (n, 1)))
@@ -502,6 +508,36 @@ def test_full_size_c2_c3_round_trip(codec, O, rebuild_path):
     codec.rebuild(k, m, sp, d, lp, out2)
     codec.synchronize()
     assert torch.equal(out2, p)
+
+
+@pytest.mark.parametrize("k,m", [(16, 4), (10, 4)])
+def test_full_size_small_block_rebuild(codec, O, k, m):
+    """bench.py's rebuild_small batches at full size: 1,048,576 x 4 KiB
+    blocks, 4 random erasures each (every block its own decode rows), the
+    WHOLE batch against the oracle (vectorised encode; per-block decode rows
+    by the oracle + vectorised MAC) on the default rebuild path."""
+    B, n, e = 4096, 1 << 20, 4
+    S = O.shard_size(B, k)
+    d = fill(codec, 0, n, B, k, S)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    s, l = ec_erasures(n, k, m, e)
+    sd, ld = dev(s), dev(l)
+    surv = empty(n, k * S)
+    codec.gather_shards(k, m, S, n, d, p, sd, surv)
+    out = empty(n, e * S)
+    codec.rebuild(k, m, sd, surv, ld, out)
+    codec.synchronize()
+    del surv
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    assert np.array_equal(host(d), data)
+    del d
+    par, _ = O.encode_simd(k, m, S, data, threads=16)
+    assert np.array_equal(host(p), par)
+    del p
+    hs = O.gather(k, m, S, data, par, s)
+    want, _ = O.rebuild_simd(k, m, S, s, hs, l, threads=16)
+    assert np.array_equal(host(out), want)
 
 
 def ec_erasures(n, k, m, e):
