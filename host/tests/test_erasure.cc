@@ -762,6 +762,25 @@ TEST(multi_device_split_matches_single, true) {
     CHECK(std::memcmp(&o1[(b * 2) * S], &data[(b * k) * S], S) == 0);
     CHECK(std::memcmp(&o1[(b * 2 + 1) * S], &p1[(b * m + 2) * S], S) == 0);
   }
+  // the mixed-geometry call split the same way: every device takes its
+  // share of each segment (per-block blocks 0..36 with e = 2; the same
+  // blocks as a shared-pattern segment with e = 1, shard 12 only)
+  Buffer s1(n * S), s3(n * S);
+  const uint8_t pat_s[10] = {1, 2, 3, 4, 5, 6, 7, 8, 9, 10}, pat_l[1] = {12};
+  for (Codec* c : {&one, &three}) {
+    Buffer& so = c == &one ? s1 : s3;
+    Buffer& po = c == &one ? o1 : o3;
+    std::fill(po.begin(), po.end(), 0);
+    memo_ec_rebuild_segment segs[2] = {
+        {k, m, S, (size_t)n, sidx.data(), surv.data(), lidx.data(), 2, 0, po.data()},
+        {k, m, S, (size_t)n, pat_s, surv.data(), pat_l, 1, 1, so.data()}};
+    c->rebuild_segments(std::vector<memo_ec_rebuild_segment>(segs, segs + 2));
+  }
+  CHECK(o1 == o3 && s1 == s3);
+  for (int b = 0; b < n; ++b) {
+    CHECK(std::memcmp(&o1[(b * 2) * S], &data[(b * k) * S], S) == 0);
+    CHECK(std::memcmp(&s1[b * S], &p1[(b * m + 2) * S], S) == 0);
+  }
 }
 
 

@@ -127,6 +127,14 @@ struct DecodeArgs {
   uint32_t stage;         // 1: exact-k rows staged through LDS
 };
 
+// Decode rows of up to MEMO_EC_MAX_SEGMENTS segments in one launch: the
+// workgroups of segment s start at wg_begin[s].
+struct DecodeLaunch {
+  uint32_t nseg;
+  uint32_t wg_begin[MEMO_EC_MAX_SEGMENTS];
+  DecodeArgs seg[MEMO_EC_MAX_SEGMENTS];
+};
+
 struct Sha256Args {
   const uint8_t* prefix;  // message i = prefix + i*prefix_stride (prefix_len B) || msg_i
   const uint8_t* msg;     // msg_i = msg + i*msg_stride, msg_len[i] (or uniform_len) bytes
@@ -160,6 +168,7 @@ hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid
 // LW0 table of (k, m) for the fused rebuild: 128 bytes (entries i < k + m).
 void lw0_host(int k, int m, uint8_t* out);
 hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st);  // closed-form decode rows
+hipError_t launch_decode_multi(const DecodeArgs* a, int n, hipStream_t st);  // several segments
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);
 hipError_t launch_sha256(const Sha256Args& a, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);

@@ -30,6 +30,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "ec_kernels.h"
 
 namespace memo_ec {
@@ -416,22 +419,52 @@ __device__ __forceinline__ uint32_t coef_sets(const MacSeg& sg, const Unit& u) {
 // Register-staged coefficient loads for the hot path (issued before the
 // shard loads; vmcnt retires in order), then the images into LDS.  Lane t
 // owns slots t + 256q, so each image store instruction covers consecutive
-// slots.
+// slots.  The loads are unconditional, at a clamped (dense rows) or dummy
+// (padding slot) offset: a load under a divergent branch whose other side
+// writes the same register makes the compiler wait for it right there
+// (vmcnt(0)), which serialised these loads, one memory latency each, in
+// front of the shard loads.  Padding slots are zeroed in store_images,
+// after the shard loads are out.
+template <int R, int KP>
+__device__ __forceinline__ bool coef_slot_ok(const MacSeg& sg, uint32_t ci, uint32_t total) {
+  if (sg.coef_dense) return ci < total;
+  const uint32_t rem = ci % (R * KP), i = rem / KP, j = rem - i * KP;
+  return ci < total && i < sg.coef_rows && j < sg.kin;
+}
 template <int R, int KP>
 __device__ __forceinline__ void load_coefs(const MacSeg& sg, const Unit& u,
                                            uint32_t (&cv)[MAC_COEF_REGS]) {
   const uint32_t total = coef_sets(sg, u) * (R * KP);
+  const uint32_t tid = threadIdx.x;
+  if (sg.coef_dense) {  // uniform: the tile's rows are one contiguous range
+    const uint8_t* base = sg.coef + u.b_first * sg.coef_bstride;
 #pragma unroll
-  for (int q = 0; q < MAC_COEF_REGS; ++q) {
-    const uint32_t ci = threadIdx.x + 256u * q;
-    cv[q] = ci < total ? coef_at<R>(sg, u, ci, KP) : 0u;
+    for (int q = 0; q < MAC_COEF_REGS; ++q) {
+      const uint32_t ci = tid + 256u * q;
+      cv[q] = base[ci < total ? ci : total - 1u];
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < MAC_COEF_REGS; ++q) {
+      const uint32_t ci = tid + 256u * q;
+      const uint32_t set = ci / (R * KP), rem = ci - set * (R * KP);
+      const uint32_t i = rem / KP, j = rem - i * KP;
+      const uint64_t off = coef_slot_ok<R, KP>(sg, ci, total)
+                               ? (u.b_first + set) * sg.coef_bstride + i * sg.kin + j
+                               : 0u;
+      cv[q] = sg.coef[off];
+    }
   }
 }
 template <int R, int KP>
 __device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
-                                             const uint32_t (&cv)[MAC_COEF_REGS], uint32_t* s_tab) {
+                                             const uint32_t (&cv0)[MAC_COEF_REGS], uint32_t* s_tab) {
   const uint32_t total = coef_sets(sg, u) * (R * KP);
   const uint32_t t = threadIdx.x;
+  uint32_t cv[MAC_COEF_REGS];
+#pragma unroll
+  for (int q = 0; q < MAC_COEF_REGS; ++q)
+    cv[q] = coef_slot_ok<R, KP>(sg, t + 256u * q, total) ? cv0[q] : 0u;
   if constexpr (MAC_COEF4) {
     static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
     if (t < total) {  // waves past the tile's slots skip the build
@@ -988,6 +1021,16 @@ gf_rebuild_kernel(const MacLaunch L) {
 // against the oracle's
 // Gauss-Jordan rows (tests/test_gpu_parity.py).
 
+// The segment of a multi-segment decode launch workgroup blockIdx.x works
+// on, and its workgroup index within that segment.
+__device__ __forceinline__ DecodeArgs dec_seg(const DecodeLaunch& L, uint32_t& bid) {
+  uint32_t sid = 0;
+  for (uint32_t i = 1; i < L.nseg; ++i)
+    if (blockIdx.x >= L.wg_begin[i]) sid = i;
+  bid = blockIdx.x - L.wg_begin[sid];
+  return L.seg[sid];
+}
+
 // LW0(i) = log sigma(i) - log Pall(i) for i < k + m, into LDS.
 __device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_t nt,
                                           uint32_t* s_lw0) {
@@ -1006,7 +1049,9 @@ __device__ __forceinline__ void stage_lw0(const uint8_t* lg, uint32_t k, uint32_
 }
 
 template <int KMAX>
-__global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(256) decode_coef_kernel(const DecodeLaunch DL) {
+  uint32_t bid;
+  const DecodeArgs a = dec_seg(DL, bid);
   __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   __shared__ uint8_t s_comp[MEMO_EC_MAX_M][256];
@@ -1015,7 +1060,7 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(DecodeArgs a) {
   const uint8_t* ex = lg + 256;
   const uint32_t k = a.k, m = a.m, e = a.e, nt = a.k + a.m;
   const uint32_t tid = threadIdx.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t b0 = (uint64_t)bid * 256;
   const uint64_t b = b0 + tid;
   const bool live = b < a.n;
   // The block's indices are loaded first, so their latency overlaps the
@@ -1188,7 +1233,9 @@ constexpr int kDecDwords = sizeof(DecTables) / 4;
 __device__ __forceinline__ uint32_t fold255(uint32_t x) { return (x & 0xFFu) + (x >> 8); }
 
 template <int K>
-__global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch DL) {
+  uint32_t bid;
+  const DecodeArgs a = dec_seg(DL, bid);
   static_assert(K <= 16, "one 32-bit survivor mask: K + MEMO_EC_MAX_M <= 32");
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kDecDwords];
   __shared__ uint32_t s_lw0[32];
@@ -1199,7 +1246,7 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
   const uint8_t* lw0 = reinterpret_cast<const uint8_t*>(s_lw0);
   const uint32_t m = a.m, e = a.e, nt = K + a.m;
   const uint32_t tid = threadIdx.x;
-  const uint64_t b0 = (uint64_t)blockIdx.x * 256;
+  const uint64_t b0 = (uint64_t)bid * 256;
   const uint64_t b = b0 + tid;
   const bool live = b < a.n;
   // The block's indices, with the widest loads their alignment allows (the
@@ -1419,14 +1466,16 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(DecodeArgs a) {
 // kernel's k * m + e * (m + 2k) in one lane: a few microseconds for a
 // C3-sized batch instead of ~15.
 template <int L>
-__global__ void __launch_bounds__(256) decode_coef_wide_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunch DL) {
+  uint32_t bid;
+  const DecodeArgs a = dec_seg(DL, bid);
   __shared__ __attribute__((aligned(16))) uint32_t s_gf[kGfDwords];
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
   const uint32_t k = a.k, e = a.e, nt = a.k + a.m, ek = a.e * a.k;
   const uint32_t t = threadIdx.x % L;
-  const uint64_t b = (uint64_t)blockIdx.x * (256 / L) + threadIdx.x / L;
+  const uint64_t b = (uint64_t)bid * (256 / L) + threadIdx.x / L;
   const bool live = b < a.n;  // whole groups
   const bool col = t < k;
   // The block's indices are loaded first, so their latency overlaps the
@@ -1773,24 +1822,30 @@ hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid
   }
 }
 
-hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
-  DecodeArgs a = a0;
-  if (a.n == 0) return hipSuccess;
+// Kernel choice for one decode segment: kind (0 column-per-lane, 1 exact-k,
+// 2 generic), its template parameter, workgroups, and the args as the
+// kernel takes them (row-staging pitch set).
+struct DecodePick {
+  int kind = 0, param = 0;
+  uint32_t grid = 0;
+  size_t lds = 0;
+  DecodeArgs a{};
+};
+
+static DecodePick decode_pick(const DecodeArgs& a0) {
+  DecodePick p;
+  p.a = a0;
+  DecodeArgs& a = p.a;
   // Small batches are latency-bound: one lane per survivor column
   // (a.wide_max: the ctx's MEMO_EC_OPT_DECODE_WIDE_MAX).
   if (a.n <= a.wide_max) {
     const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
-    const uint32_t g = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
-    switch (L) {
-      case 4: hipLaunchKernelGGL(decode_coef_wide_kernel<4>, dim3(g), dim3(256), 0, st, a); break;
-      case 8: hipLaunchKernelGGL(decode_coef_wide_kernel<8>, dim3(g), dim3(256), 0, st, a); break;
-      case 16: hipLaunchKernelGGL(decode_coef_wide_kernel<16>, dim3(g), dim3(256), 0, st, a); break;
-      case 32: hipLaunchKernelGGL(decode_coef_wide_kernel<32>, dim3(g), dim3(256), 0, st, a); break;
-      default: hipLaunchKernelGGL(decode_coef_wide_kernel<64>, dim3(g), dim3(256), 0, st, a); break;
-    }
-    return hipGetLastError();
+    p.kind = 0;
+    p.param = (int)L;
+    p.grid = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
+    return p;
   }
-  const uint32_t grid = (uint32_t)((a.n + 255) / 256);
+  p.grid = (uint32_t)((a.n + 255) / 256);
   // LDS staging of the rows: pitch = e*k rounded up to an odd dword count
   const uint32_t ek = a.e * a.k;
   uint32_t pw = (ek + 3) / 4;
@@ -1800,36 +1855,84 @@ hipError_t launch_decode_coef(const DecodeArgs& a0, hipStream_t st) {
   // exact-k kernels for the common codes, k in {2, 3, 4, 6, 8, 10, 12, 14,
   // 16} (a.exact), storing whole-dword rows straight from registers unless
   // a.stage asks for the LDS staging (A/B runs and tests)
-  const bool exact = a.exact != 0;
-  const bool stage = a.stage != 0;
   DecodeArgs ax = a;
-  if (!stage && (ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) ax.pitch = 0;
-  if (exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32) {
-    const size_t xlds = ax.pitch ? lds : 0;
-    switch (a.k) {
-#define MEMO_EC_DK(x)                                                                    \
-  case x:                                                                                \
-    hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), xlds, st, ax);    \
-    return hipGetLastError();
+  if (!a.stage && (ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) ax.pitch = 0;
+  const bool exact_k = a.k == 2 || a.k == 3 || a.k == 4 || a.k == 6 || a.k == 8 || a.k == 10 ||
+                       a.k == 12 || a.k == 14 || a.k == 16;
+  if (a.exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32 && exact_k) {
+    p.kind = 1;
+    p.param = (int)a.k;
+    p.lds = ax.pitch ? lds : 0;
+    p.a = ax;
+    return p;
+  }
+  p.kind = 2;
+  p.param = a.k <= 4 ? 4 : a.k <= 10 ? 10 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
+  p.lds = lds;
+  return p;
+}
+
+static hipError_t decode_launch(int kind, int param, const DecodeLaunch& L, uint32_t grid, size_t lds,
+                                hipStream_t st) {
+  if (kind == 0) {
+    switch (param) {
+      case 4: hipLaunchKernelGGL(decode_coef_wide_kernel<4>, dim3(grid), dim3(256), 0, st, L); break;
+      case 8: hipLaunchKernelGGL(decode_coef_wide_kernel<8>, dim3(grid), dim3(256), 0, st, L); break;
+      case 16: hipLaunchKernelGGL(decode_coef_wide_kernel<16>, dim3(grid), dim3(256), 0, st, L); break;
+      case 32: hipLaunchKernelGGL(decode_coef_wide_kernel<32>, dim3(grid), dim3(256), 0, st, L); break;
+      default: hipLaunchKernelGGL(decode_coef_wide_kernel<64>, dim3(grid), dim3(256), 0, st, L); break;
+    }
+  } else if (kind == 1) {
+    switch (param) {
+#define MEMO_EC_DK(x) \
+  case x: hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), lds, st, L); break;
       MEMO_EC_DK(2) MEMO_EC_DK(3) MEMO_EC_DK(4) MEMO_EC_DK(6) MEMO_EC_DK(8) MEMO_EC_DK(10)
       MEMO_EC_DK(12) MEMO_EC_DK(14) MEMO_EC_DK(16)
 #undef MEMO_EC_DK
-      default: break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (param) {
+      case 4: hipLaunchKernelGGL(decode_coef_kernel<4>, dim3(grid), dim3(256), lds, st, L); break;
+      case 10: hipLaunchKernelGGL(decode_coef_kernel<10>, dim3(grid), dim3(256), lds, st, L); break;
+      case 16: hipLaunchKernelGGL(decode_coef_kernel<16>, dim3(grid), dim3(256), lds, st, L); break;
+      case 32: hipLaunchKernelGGL(decode_coef_kernel<32>, dim3(grid), dim3(256), lds, st, L); break;
+      default: hipLaunchKernelGGL(decode_coef_kernel<64>, dim3(grid), dim3(256), lds, st, L); break;
     }
   }
-  if (a.k <= 4)
-    hipLaunchKernelGGL(decode_coef_kernel<4>, dim3(grid), dim3(256), lds, st, a);
-  else if (a.k <= 10)
-    hipLaunchKernelGGL(decode_coef_kernel<10>, dim3(grid), dim3(256), lds, st, a);
-  else if (a.k <= 16)
-    hipLaunchKernelGGL(decode_coef_kernel<16>, dim3(grid), dim3(256), lds, st, a);
-  else if (a.k <= 32)
-    hipLaunchKernelGGL(decode_coef_kernel<32>, dim3(grid), dim3(256), lds, st, a);
-  else
-    hipLaunchKernelGGL(decode_coef_kernel<64>, dim3(grid), dim3(256), lds, st, a);
   return hipGetLastError();
 }
 
+// Decode rows of several segments: segments that take the same kernel share
+// a launch (up to MEMO_EC_MAX_SEGMENTS each), so a mixed rebuild's many
+// small decodes fill the chip together instead of one after another.
+hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
+  std::vector<DecodePick> picks;
+  for (int i = 0; i < na; ++i)
+    if (as[i].n) picks.push_back(decode_pick(as[i]));
+  std::vector<bool> done(picks.size(), false);
+  for (size_t i = 0; i < picks.size(); ++i) {
+    if (done[i]) continue;
+    DecodeLaunch L{};
+    uint64_t wg = 0;
+    size_t lds = 0;
+    for (size_t j = i; j < picks.size() && L.nseg < MEMO_EC_MAX_SEGMENTS; ++j) {
+      const DecodePick& p = picks[j];
+      if (done[j] || p.kind != picks[i].kind || p.param != picks[i].param) continue;
+      if (L.nseg && wg + p.grid > 0x7fffffffull) break;
+      done[j] = true;
+      L.wg_begin[L.nseg] = (uint32_t)wg;
+      L.seg[L.nseg++] = p.a;
+      wg += p.grid;
+      lds = std::max(lds, p.lds);
+    }
+    if (wg > 0x7fffffffull) return hipErrorInvalidValue;
+    if (hipError_t e = decode_launch(picks[i].kind, picks[i].param, L, (uint32_t)wg, lds, st)) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st) { return launch_decode_multi(&a, 1, st); }
 
 hipError_t launch_fill(const FillArgs& a, hipStream_t st) {
   const uint64_t total = a.n * (a.stride / 16);

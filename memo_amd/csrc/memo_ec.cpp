@@ -950,17 +950,19 @@ int plan_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segmen
 int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t* rows,
                           hipStream_t st, uint32_t* status) {
   std::vector<const uint8_t*> prow(ps.size(), nullptr);
+  std::vector<DecodeArgs> dec;
   size_t off = 0;
   for (size_t i = 0; i < ps.size(); ++i) {
     const auto& p = ps[i];
     if (p.mode != MAC_ROWS) continue;
     const uint32_t* lw0 = nullptr;
     if (int rc = lw0_table(c, p.k, p.m, &lw0)) return rc;
-    const DecodeArgs a = decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0);
-    HIPCHK(launch_decode_coef(a, st));
+    dec.push_back(decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0));
     prow[i] = rows + off;
     off += p.n * (size_t)p.e * p.k;
   }
+  // every segment's decode rows, segments of one decode kernel per launch
+  if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
   std::vector<bool> done(ps.size(), false);
   for (size_t i = 0; i < ps.size(); ++i) {
     if (done[i]) continue;

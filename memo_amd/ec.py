@@ -337,6 +337,7 @@ class Codec:
             raise ValueError("surv and out must both be device or both host buffers")
         si = np.ascontiguousarray(np.asarray(surv_idx, dtype=np.uint8).reshape(-1))
         li = np.ascontiguousarray(np.asarray(lost_idx, dtype=np.uint8).reshape(-1))
+        _check_pattern(si, li, k, m)
         if S is None:
             n, S = _infer_nS(surv, k)
         where = DEVICE if sw == DEVICE else (HOST_PINNED if sw == ow == HOST_PINNED else HOST)
@@ -366,6 +367,7 @@ class Codec:
             if uni:
                 si = np.ascontiguousarray(np.asarray(s["surv_idx"], dtype=np.uint8).reshape(-1))
                 li = np.ascontiguousarray(np.asarray(s["lost_idx"], dtype=np.uint8).reshape(-1))
+                _check_pattern(si, li, k, m)
                 keep += [si, li]
                 ip, lp, e = si.ctypes.data, li.ctypes.data, len(li)
             else:
@@ -415,6 +417,15 @@ class Codec:
         _check(_lib().memo_ec_gather_shards(self._ctx, k, m, S, n, _ptr(data)[0], _ptr(parity)[0],
                                             _ptr(idx)[0], cnt, _ptr(out)[0]), "gather_shards")
         return out
+
+
+def _check_pattern(si, li, k, m):
+    """A shared erasure pattern: the C side reads exactly k survivor and e
+    lost indices from these host arrays, so their lengths are checked here."""
+    if len(si) != k:
+        raise ValueError("surv_idx has %d entries, k = %d" % (len(si), k))
+    if not 1 <= len(li) <= m:
+        raise ValueError("lost_idx has %d entries, need 1..m = %d" % (len(li), m))
 
 
 def _infer_nS(buf, k):

@@ -76,3 +76,22 @@ def test_no_gpu_fails_loudly():
     from memo_amd import ec
     with pytest.raises(ec.MemoECError):
         ec.Codec(0)
+
+
+def test_shared_pattern_lengths_checked():
+    """rebuild_uniform / shared-pattern segments: the C side reads exactly k
+    and e host indices, so short sequences are refused before the call (no
+    GPU needed: the check comes first)."""
+    from memo_amd import ec
+    import numpy as np
+    c = ec.Codec.__new__(ec.Codec)  # no ctx: the check must raise before any call
+    buf = np.zeros((2, 10 * 64), np.uint8)
+    out = np.zeros((2, 64), np.uint8)
+    with pytest.raises(ValueError):
+        c.rebuild_uniform(10, 4, [0, 1, 2], buf, [12], out)
+    with pytest.raises(ValueError):
+        c.rebuild_uniform(10, 4, list(range(10)), buf, [], out)
+    with pytest.raises(ValueError):
+        c.rebuild_uniform(10, 4, list(range(10)), buf, [10, 11, 12, 13, 9], out)
+    with pytest.raises(ValueError):
+        c.rebuild_segments([dict(k=10, m=4, surv=buf, out=out, uniform=True, surv_idx=[0], lost_idx=[12])])
