@@ -59,6 +59,7 @@ extern "C" {
 #define MEMO_EC_MAX_M 16
 #define MEMO_EC_MAX_SEGMENTS 12          /* memo_ec_encode_segments  */
 #define MEMO_EC_MAX_REBUILD_SEGMENTS 256 /* memo_ec_rebuild_segments */
+/* Shards are shorter than 4 GiB (S < 2^32; MEMO_EC_ERANGE otherwise). */
 
 typedef struct memo_ec_ctx memo_ec_ctx;
 

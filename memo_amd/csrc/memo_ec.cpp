@@ -85,6 +85,9 @@ struct memo_ec_ctx {
 namespace {
 
 constexpr size_t kLdsBudget = 48 * 1024;  // table LDS per workgroup (flat mapping)
+// Largest shard (a documented limit: 2^32 bytes, far above any block memo
+// stores; the kernels' column indices are 32-bit).
+constexpr size_t kMaxShard = (size_t)1 << 32;
 
 int hip_rc(hipError_t e) {
   if (e == hipSuccess) return MEMO_EC_OK;
@@ -893,6 +896,7 @@ int plan_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segmen
     if (s.e < 0 || s.e > s.m) return MEMO_EC_EINVAL;
     if (s.e == 0 || s.n == 0) continue;
     if (s.S == 0 || s.S % 64 || !s.surv_idx || !s.surv || !s.lost_idx || !s.out) return MEMO_EC_EINVAL;
+    if (s.S >= kMaxShard) return MEMO_EC_ERANGE;
     RPiece p;
     p.seg = i;
     p.k = s.k;
@@ -1172,6 +1176,7 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   if (int rc = check_km(k, m)) return rc;
   if (m == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !data || !parity) return MEMO_EC_EINVAL;
+  if (S >= kMaxShard) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   if (where == MEMO_EC_DEVICE) return encode_device(c, k, m, S, n, data, parity, c->stream);
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
@@ -1202,6 +1207,7 @@ int memo_ec_rebuild_uniform(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e < 0 || e > m) return MEMO_EC_EINVAL;
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
+  if (S >= kMaxShard) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   const int R = mac_rbound(e), KC = mac_kchunk(k, R);
   const uint32_t* tab = nullptr;
@@ -1246,6 +1252,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e < 0 || e > m) return MEMO_EC_EINVAL;
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
+  if (S >= kMaxShard) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   const bool fused = rebuild_fused(c, n * (size_t)k * S);
   if (where == MEMO_EC_DEVICE) {
@@ -1370,6 +1377,7 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
     if (segs[i].m == 0 || segs[i].n == 0) continue;
     if (segs[i].S == 0 || segs[i].S % 64 || !segs[i].data || !segs[i].parity)
       return MEMO_EC_EINVAL;
+    if (segs[i].S >= kMaxShard) return MEMO_EC_ERANGE;
     if (segs[i].n > max_blocks_per_launch(c, segs[i].S)) return MEMO_EC_ERANGE;
     const int kc = mac_kchunk(segs[i].k, mac_rbound(segs[i].m));
     size_t ci = 0;
