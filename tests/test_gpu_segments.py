@@ -96,8 +96,10 @@ def test_mixed_rebuild_host_memory(codec, O, pinned, mode, rebuild_path):
         out = (torch.zeros((g["n"], g["e"] * g["S"]), dtype=torch.uint8).pin_memory() if pinned
                else np.zeros((g["n"], g["e"] * g["S"]), np.uint8))
         d = dict(k=g["k"], m=g["m"], surv=surv, out=out, uniform=g["uniform"])
-        d.update(surv_idx=g["su"], lost_idx=g["lu"]) if g["uniform"] else d.update(surv_idx=g["s"],
-                                                                                    lost_idx=g["l"])
+        if g["uniform"]:
+            d.update(surv_idx=g["su"], lost_idx=g["lu"])
+        else:
+            d.update(surv_idx=g["s"], lost_idx=g["l"])
         segs.append(d)
     with codec.options(**opts):
         codec.rebuild_segments(segs)
@@ -169,3 +171,23 @@ def test_segments_bad_patterns(codec, O, rebuild_path):
     codec.rebuild_segments([dict(k=10, m=4, surv=empty(0, 640), out=empty(0, 64), n=0, S=64,
                                  surv_idx=empty(0, 10), lost_idx=empty(0, 1))])
     codec.synchronize()
+
+
+@pytest.mark.parametrize("spec", [
+    # k outside the straight-line bodies (chunk loop), k > 16, m > 4 (R > 4)
+    [(3, 2, 5000, 9, 2, False), (5, 3, 4096, 20, 3, False), (7, 3, 70000, 4, 1, True),
+     (20, 4, 300000, 3, 4, False), (33, 12, 9000, 5, 12, False), (12, 1, 4096, 40, 1, False)],
+    # KC = 6 / 12 / 14 (R <= 4) beside R > 4 groups of the 4-shard chunk class
+    [(6, 3, 4096, 30, 3, False), (6, 6, 30000, 3, 6, False), (12, 4, 70000, 2, 4, True),
+     (14, 2, 4096, 25, 2, False), (4, 8, 8192, 7, 8, False), (12, 5, 999, 7, 5, False)],
+])
+def test_mixed_codes_any_k(codec, O, spec, rebuild_path):
+    """Mixed codes in one call beyond the C5 mix: k in the chunk loop and
+    above 16, m > 4 (R > 4 classes), the k = 6 / 12 / 14 bodies beside R > 4
+    groups, per-block and shared patterns."""
+    groups = make_groups(O, spec, 6)
+    segs = device_segs(groups)
+    codec.rebuild_segments(segs)
+    codec.synchronize()
+    for g, s in zip(groups, segs):
+        assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (g["k"], g["m"], g["S"], g["e"])
