@@ -905,3 +905,28 @@ def test_rebuild_uniform_invalid_and_cache(codec, O):
                               lost, o)
         codec.synchronize()
         assert np.array_equal(host(o), O.gather(k, m, S, data, par, np.tile(lost, (n, 1)))), i
+
+
+def test_ctx_options_round_trip(codec):
+    """memo_ec_ctx_set_option / get_option: every option reads back what was
+    set, out-of-range values and unknown options are refused (EINVAL) and
+    leave the option unchanged, and a fresh ctx starts from the environment
+    defaults, not from another ctx's settings."""
+    from memo_amd import ec
+    values = {"rebuild_path": 0, "fused_max_bytes": 1 << 20, "zero_copy_bytes": 0,
+              "pipe_bytes": 8 << 20, "copy_threads": 2, "max_launch_tiles": 1000,
+              "xcd_min_tiles": 1, "decode_wide_max": 0, "decode_exact": 0, "decode_stage": 1}
+    old = {k: codec.get_option(k) for k in values}
+    with codec.options(**values):
+        assert {k: codec.get_option(k) for k in values} == values
+        with ec.Codec(0) as fresh:
+            assert {k: fresh.get_option(k) for k in values} == old
+    assert {k: codec.get_option(k) for k in values} == old
+    for name, bad in [("rebuild_path", 2), ("rebuild_path", -2), ("pipe_bytes", 1000),
+                      ("decode_exact", 3), ("copy_threads", -1)]:
+        with pytest.raises(ec.MemoECError) as ei:
+            codec.set_option(name, bad)
+        assert ei.value.code == -1
+        assert codec.get_option(name) == old[name]
+    L = ec._lib()
+    assert L.memo_ec_ctx_set_option(codec._ctx, 99, 0) == -1
