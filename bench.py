@@ -81,6 +81,15 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+def log(msg):
+    """Progress on stderr (stdout carries only the JSON line): long runs keep
+    showing signs of life."""
+    print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+
+
+_T0 = time.perf_counter()
+
+
 def timed_steps(torch, fns, steps, warmup, settle_ms, dist, stream):
     """`warmup` untimed steps (continued until settle_ms of wall time has gone
     by), then exactly `steps` steps bracketed by barrier + synchronize.  A
@@ -195,6 +204,7 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
                 pt["cpu_threads"] = th
                 pt["cpu_bit_exact"] = ok
             points.append(pt)
+            log("sweep RS(%d,%d) %d B: encode %.3f, rebuild %.3f" % (k, m, B, pt["frac"], pt["rebuild"]["frac"]))
             del d, p, surv, want, out, sd, ld
     segs, rsegs, checks, alg, ralg, pay = [], [], [], 0, 0, 0
     for gi, (k, m) in enumerate([(4, 2), (10, 4), (16, 4)]):
@@ -745,6 +755,7 @@ def main():
         fns.append(lambda: codec.rebuild(k, m, sd, surv, ld, out))
     torch.cuda.synchronize()
 
+    log("rank %d: inputs resident, timing %d steps" % (rank, args.steps))
     wall, kms, done = timed_steps(torch, fns, args.steps, args.warmup, args.settle_ms, dist, stream)
     codec.synchronize()
     row = {"rank": rank, "device": local, "warmup_steps_run": done,
@@ -795,14 +806,17 @@ def main():
         extras = [None] * world
         dist.all_gather_object(extras, extra)
     merge_extras(result, extras)
+    log("rank %d: timed steps done, side measurements" % rank)
     if world == 1 and not args.no_small:
         result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps,
                                                 args.warmup, args.settle_ms)
     if rank == 0:
         if not args.no_cpu:
+            log("cpu baseline")
             result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, par[:4].cpu().numpy())
             result["c1"] = c1_case(torch, ec, codec, stream)
         if not args.no_pmc:
+            log("counter passes")
             pmc_traffic(args, result, local, world)
         if args.sha:
             result["sha256"] = sha_lines(torch, codec, stream, data, n, B)
