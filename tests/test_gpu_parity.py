@@ -278,6 +278,36 @@ def test_one_huge_ragged_block(codec, O):
     assert np.array_equal(host(out), O.gather(k, m, S, data, want, l))
 
 
+def test_block_beyond_32bit_offsets(codec, O):
+    """One 5 GiB + 3 byte RS(2,1) block: S = 2.5 GiB (above 2^31), the
+    second data shard and the block's end past 2^32 bytes, so every shard
+    and column offset needs 64 bits.  Encode, then rebuild data shard 0 from
+    (data shard 1, parity) on both rebuild paths, whole shards against the
+    oracle."""
+    k, m, B, n = 2, 1, (5 << 30) + 3, 1
+    S = O.shard_size(B, k)
+    assert S > (1 << 31) and k * S > (1 << 32)
+    data = O.fill_blocks(SEED, 77, n, B, k, S)
+    par, _ = O.encode_simd(k, m, S, data, threads=16)
+    d = empty(n, k * S)
+    codec.fill_blocks(SEED, 77, n, B, k, S, d)
+    p = empty(n, m * S)
+    codec.encode(k, m, d, p)
+    codec.synchronize()
+    assert np.array_equal(host(p), par)
+    s, l = np.array([[1, 2]], np.uint8), np.array([[0]], np.uint8)
+    surv = empty(n, k * S)
+    codec.gather_shards(k, m, S, n, d, p, dev(s), surv)
+    del d, p
+    for path in (0, 1):
+        out = empty(n, S)
+        with codec.options(rebuild_path=path):
+            codec.rebuild(k, m, dev(s), surv, dev(l), out)
+            codec.synchronize()
+        assert np.array_equal(host(out)[0], data[0, :S]), path
+        del out
+
+
 def test_small_blocks_many_per_tile(codec, O, rebuild_path):
     # 4 KiB blocks with k=16: S=256, 16 columns per block, tables for ~17
     # blocks per tile in the rebuild kernel.
