@@ -5,6 +5,8 @@
 # way into memo_amd/_lib/asan/ next to the in-tree kernels object; then (on
 # the GPU box) runs the plugin tests against that library.
 #   tools/host_asan.sh build    (here)    tools/host_asan.sh run   (GPU box)
+# The two sanitizer builds are listed in .gpurunignore (they are large and
+# no round-end run loads them): drop those two lines for a call that runs it.
 set -e
 cd "$(dirname "$0")/../host"
 if [ "$1" = build ]; then
