@@ -114,7 +114,7 @@ enum memo_ec_option {
                                            0 decode rows + MAC, 1 fused kernel   */
     MEMO_EC_OPT_FUSED_MAX_BYTES = 2,    /* MEMO_EC_FUSED_MAX_MB: auto takes the fused
                                            kernel up to this many survivor bytes
-                                           per call (64 MiB)                     */
+                                           per call (256 MiB)                    */
     MEMO_EC_OPT_ZERO_COPY_BYTES = 3,    /* MEMO_EC_ZC_KB: host calls moving at most
                                            this many bytes run their kernels on
                                            pinned host memory (4 MiB; 0: off)    */

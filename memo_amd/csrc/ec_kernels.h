@@ -37,6 +37,12 @@
 #ifndef MEMO_EC_MAC_PAIR16
 #define MEMO_EC_MAC_PAIR16 1
 #endif
+// The same for the k = 16 bodies with per-block tables (rebuild MAC and
+// fused rebuild): pairing takes them from 124 to 153 VGPRs (4 -> 3 waves
+// per SIMD)
+#ifndef MEMO_EC_MAC_PAIR16_COEF
+#define MEMO_EC_MAC_PAIR16_COEF 1
+#endif
 
 namespace memo_ec {
 

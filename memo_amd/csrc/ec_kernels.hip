@@ -175,7 +175,7 @@ __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d
                                           const TabRef<SOA>& tab, uint32_t kpad, uint32_t j0) {
   // Pairing costs 12 selector VGPRs: the k = 16 body keeps 4 waves per
   // SIMD only without it (MEMO_EC_MAC_PAIR16).
-  constexpr bool PAIR = MAC_PAIR && (KC != 16 || MEMO_EC_MAC_PAIR16);
+  constexpr bool PAIR = MAC_PAIR && (KC != 16 || (SOA ? MEMO_EC_MAC_PAIR16_COEF : MEMO_EC_MAC_PAIR16));
 #pragma unroll
   for (int g = 0; g < KC; g += PAIR ? 2 : 1) {
     const bool two = PAIR && g + 1 < KC;
@@ -1215,7 +1215,9 @@ __global__ void __launch_bounds__(256) decode_coef_kernel(const DecodeLaunch DL)
 // EX is 2^(i mod 255) over 1280 entries.  Duplicate and out-of-range
 // indices are found from the mask and an OR of all indices (no per-index
 // tests); a faulty block's rows are zeroed once at the end.  Same results
-// as decode_coef_kernel (tests/test_gpu_parity.py).
+// as decode_coef_kernel (tests/test_gpu_parity.py).  MM bounds m (4 or
+// MEMO_EC_MAX_M): the per-lane lists of lost and non-survivor indices are MM
+// long, so the m <= 4 codes keep fewer registers live.
 struct DecTables {
   uint8_t lg[256];    // log
   uint8_t nlg[256];   // 255 - log (nlg[0]: 0, never used for a non-unit row)
@@ -1241,11 +1243,12 @@ constexpr int kDecDwords = sizeof(DecTables) / 4;
 
 __device__ __forceinline__ uint32_t fold255(uint32_t x) { return (x & 0xFFu) + (x >> 8); }
 
-template <int K>
+template <int K, int MM>
 __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch DL) {
   uint32_t bid;
   const DecodeArgs a = dec_seg(DL, bid);
   static_assert(K <= 16, "one 32-bit survivor mask: K + MEMO_EC_MAX_M <= 32");
+  static_assert(MM % 4 == 0 && MM <= MEMO_EC_MAX_M, "m bound in groups of 4");
   __shared__ __attribute__((aligned(16))) uint32_t s_tab[kDecDwords];
   __shared__ uint32_t s_lw0[32];
   extern __shared__ __attribute__((aligned(16))) uint8_t s_out[];  // 256 x pitch
@@ -1260,7 +1263,7 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
   const bool live = b < a.n;
   // The block's indices, with the widest loads their alignment allows (the
   // kernel is short: its first loads are a visible part of it).
-  uint32_t sv[K], lv[MEMO_EC_MAX_M];
+  uint32_t sv[K], lv[MM];
   const uintptr_t sa = reinterpret_cast<uintptr_t>(a.surv_idx);
   if (K % 4 == 0 && (sa & 3) == 0) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(a.surv_idx + b * K);
@@ -1285,14 +1288,14 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
   if ((e & 3) == 0 && (reinterpret_cast<uintptr_t>(a.lost_idx) & 3) == 0) {
     const uint32_t* p = reinterpret_cast<const uint32_t*>(a.lost_idx + b * e);
 #pragma unroll
-    for (int w = 0; w < MEMO_EC_MAX_M / 4; ++w) {
+    for (int w = 0; w < MM / 4; ++w) {
       const uint32_t x = (live && (uint32_t)(4 * w) < e) ? p[w] : 0u;
 #pragma unroll
       for (int j = 0; j < 4; ++j) lv[4 * w + j] = (x >> (8 * j)) & 0xFFu;
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < MEMO_EC_MAX_M; ++r) lv[r] = (live && (uint32_t)r < e) ? a.lost_idx[b * e + r] : 0u;
+    for (int r = 0; r < MM; ++r) lv[r] = (live && (uint32_t)r < e) ? a.lost_idx[b * e + r] : 0u;
   }
   {
     const uint32_t* src = reinterpret_cast<const uint32_t*>(&kDec);
@@ -1304,7 +1307,7 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
   // the rows go to global memory straight from registers when they are
   // whole dwords (pitch 0, set by the launcher), else through LDS
   const bool direct = a.pitch == 0;
-  constexpr int kW = (MEMO_EC_MAX_M * K + 3) / 4;
+  constexpr int kW = (MM * K + 3) / 4;
   uint32_t wd[kW];
   if (live) {
     // survivor set: a duplicate leaves fewer than K bits, an index >= nt a
@@ -1317,16 +1320,16 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
     }
     uint32_t lany = 0;
 #pragma unroll
-    for (int r = 0; r < MEMO_EC_MAX_M; ++r)
+    for (int r = 0; r < MM; ++r)
       if ((uint32_t)r < e) lany |= lv[r] >= nt ? 1u : 0u;
     const uint32_t valid = nt >= 32 ? ~0u : (1u << nt) - 1u;
     const bool bad = (uint32_t)__popc(mask) != (uint32_t)K || (mask & ~valid) != 0 || (any >> 5) != 0 ||
                      lany != 0;
     // the m non-survivors, in registers
     uint32_t comp = ~mask & valid;
-    uint32_t cl[MEMO_EC_MAX_M];
+    uint32_t cl[MM];
 #pragma unroll
-    for (int q = 0; q < MEMO_EC_MAX_M; ++q) {
+    for (int q = 0; q < MM; ++q) {
       cl[q] = kDecNone;
       if ((uint32_t)q < m) {
         cl[q] = __builtin_ctz(comp | 0x80000000u);  // a faulty set may run out: 31
@@ -1339,7 +1342,7 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
 #pragma unroll
     for (int t = 0; t < K; ++t) lw[t] = lw0[sv[t] & 31];
 #pragma unroll
-    for (int q = 0; q < MEMO_EC_MAX_M; q += 4) {
+    for (int q = 0; q < MM; q += 4) {
       if ((uint32_t)q + 2 < m) {
 #pragma unroll
         for (int t = 0; t < K; ++t)
@@ -1358,13 +1361,13 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
     const bool vec8 = (ek & 7) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 7) == 0;
     uint32_t word = 0;
 #pragma unroll
-    for (int r = 0; r < MEMO_EC_MAX_M; ++r) {
+    for (int r = 0; r < MM; ++r) {
       if ((uint32_t)r < e) {
         const uint32_t l = lv[r] & 0xFFu;
         const bool unit = (mask >> (l & 31)) & 1u;
         uint32_t acc = lw0[l & 31];
 #pragma unroll
-        for (int q = 0; q < MEMO_EC_MAX_M; q += 4)  // c == l adds log[0] = 0
+        for (int q = 0; q < MM; q += 4)  // c == l adds log[0] = 0
           if ((uint32_t)q < m)
             acc += (lg[l ^ cl[q]] + lg[l ^ cl[q + 1]]) + (lg[l ^ cl[q + 2]] + lg[l ^ cl[q + 3]]);
         uint32_t llam = 510u - fold255(acc);  // == -log(Lam_l) mod 255, in [239, 510]
@@ -1870,7 +1873,7 @@ static DecodePick decode_pick(const DecodeArgs& a0) {
                        a.k == 12 || a.k == 14 || a.k == 16;
   if (a.exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32 && exact_k) {
     p.kind = 1;
-    p.param = (int)a.k;
+    p.param = (int)a.k + (a.m <= 4 ? 0 : 100);  // m bound 4 or MEMO_EC_MAX_M
     p.lds = ax.pitch ? lds : 0;
     p.a = ax;
     return p;
@@ -1893,8 +1896,11 @@ static hipError_t decode_launch(int kind, int param, const DecodeLaunch& L, uint
     }
   } else if (kind == 1) {
     switch (param) {
-#define MEMO_EC_DK(x) \
-  case x: hipLaunchKernelGGL(decode_rows_k_kernel<x>, dim3(grid), dim3(256), lds, st, L); break;
+#define MEMO_EC_DK(x)                                                                            \
+  case x: hipLaunchKernelGGL((decode_rows_k_kernel<x, 4>), dim3(grid), dim3(256), lds, st, L); break; \
+  case 100 + x:                                                                                   \
+    hipLaunchKernelGGL((decode_rows_k_kernel<x, MEMO_EC_MAX_M>), dim3(grid), dim3(256), lds, st, L); \
+    break;
       MEMO_EC_DK(2) MEMO_EC_DK(3) MEMO_EC_DK(4) MEMO_EC_DK(6) MEMO_EC_DK(8) MEMO_EC_DK(10)
       MEMO_EC_DK(12) MEMO_EC_DK(14) MEMO_EC_DK(16)
 #undef MEMO_EC_DK

@@ -27,7 +27,7 @@ using namespace memo_ec;
 // once at memo_ec_ctx_create, so no call reads the environment).
 struct memo_ec_opts {
   int rebuild_path = -1;                  // -1 auto, 0 decode rows + MAC, 1 fused
-  size_t fused_max_bytes = 64ull << 20;   // auto: fused up to this many survivor bytes
+  size_t fused_max_bytes = 256ull << 20;  // auto: fused up to this many survivor bytes
   size_t zc_max_bytes = 4ull << 20;       // host calls up to this many bytes: zero-copy
   size_t pipe_bytes = 64ull << 20;        // host pipeline batch
   int copy_threads = 0;                   // pageable bounce copy threads (0: all)
@@ -379,9 +379,12 @@ int lw0_table(memo_ec_ctx* ctx, int k, int m, const uint32_t** out) {
 
 // The device rebuild path of a call moving `in_bytes` of survivors:
 //  - fused (gf_rebuild_kernel: each tile derives its blocks' decode rows, one
-//    launch) for calls up to MEMO_EC_FUSED_MAX_MB (64) MiB: latency-bound,
-//    the saved launch wins (one-block degraded reads: 4 KiB 27-30 -> 23 us,
-//    1 MiB 78-88 -> 62-72 us, profiles/r02_host_latency_fused_ab.jsonl);
+//    launch) for calls up to MEMO_EC_FUSED_MAX_MB (256) MiB: a chip that
+//    is not filled twice over wins by the saved launch and rows round trip
+//    (one-block degraded reads: 4 KiB 27-30 -> 23 us, 1 MiB 78-88 -> 62-72
+//    us, profiles/r02_host_latency_fused_ab.jsonl; 16-256 MiB calls of 4 KiB
+//    or 1 MiB blocks 10-30% faster fused, equal at 420 MiB - 1 GiB,
+//    profiles/r03_fused_bound_probe.jsonl);
 //  - two kernels (decode_coef*/decode_rows_k rows through HBM, then
 //    gf_mac_kernel) above: the MAC is ~75% VALU-busy and the fused decode's
 //    VALU/LDS work costs more than the decode kernel it removes (C3 1054 vs

@@ -177,7 +177,7 @@ def erasures(seed, first_block, n, k, m, e):
 def rebuild_path(n=None, k=None, S=None):
     """Which device rebuild the library runs (memo_ec.cpp rebuild_fused):
     'fused' -- one gf_rebuild_kernel launch whose tiles derive their blocks'
-    decode rows (calls of up to MEMO_EC_FUSED_MAX_MB = 64 MiB of survivors);
+    decode rows (calls of up to MEMO_EC_FUSED_MAX_MB = 256 MiB of survivors);
     'rows' -- decode rows through HBM, then gf_mac_kernel (larger calls).
     MEMO_EC_REBUILD_FUSED=0/1 forces one."""
     v = os.environ.get("MEMO_EC_REBUILD_FUSED")
@@ -185,7 +185,7 @@ def rebuild_path(n=None, k=None, S=None):
         return "fused" if _atoi(v) != 0 else "rows"
     if None in (n, k, S):
         return "auto"
-    max_mb = _atoi(os.environ.get("MEMO_EC_FUSED_MAX_MB", "64"))
+    max_mb = _atoi(os.environ.get("MEMO_EC_FUSED_MAX_MB", "256"))
     return "fused" if n * k * S <= (max_mb << 20) else "rows"
 
 
@@ -199,7 +199,7 @@ def _atoi(v):
 def rebuild_kernel_name(n=None, k=None, S=None):
     return {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
             "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM)",
-            "auto": "fused up to 64 MiB per call, else decode rows + gf_mac_kernel"}[
+            "auto": "fused up to 256 MiB per call, else decode rows + gf_mac_kernel"}[
         rebuild_path(n, k, S)]
 
 
