@@ -59,7 +59,9 @@ extern "C" {
 #define MEMO_EC_MAX_M 16
 #define MEMO_EC_MAX_SEGMENTS 12          /* memo_ec_encode_segments  */
 #define MEMO_EC_MAX_REBUILD_SEGMENTS 256 /* memo_ec_rebuild_segments */
-/* Shards are shorter than 4 GiB (S < 2^32; MEMO_EC_ERANGE otherwise). */
+/* Shards are shorter than 4 GiB (S < 2^32), and a call's buffers hold less
+ * than 2^50 bytes (n * (k + m) * S, n * (k + e) * S; MEMO_EC_ERANGE
+ * otherwise, before anything is sized from them). */
 
 typedef struct memo_ec_ctx memo_ec_ctx;
 

@@ -207,6 +207,15 @@ void read_env_options(memo_ec_opts& o) {
   }
 }
 
+// A call moves n * per bytes of caller buffers.  Products that overflow, or
+// pass 2^50 bytes (1 PiB: beyond any device or host memory), are refused
+// with MEMO_EC_ERANGE before scratch or grids are sized from them.
+constexpr uint64_t kMaxCallBytes = 1ull << 50;
+bool too_big(size_t n, size_t per) {
+  uint64_t b = 0;
+  return __builtin_mul_overflow((uint64_t)n, (uint64_t)per, &b) || b > kMaxCallBytes;
+}
+
 int check_km(int k, int m) {
   if (k < 1 || m < 0) return MEMO_EC_EINVAL;
   if (k > MEMO_EC_MAX_K || m > MEMO_EC_MAX_M) return MEMO_EC_ERANGE;
@@ -899,7 +908,7 @@ int plan_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segmen
     if (s.e < 0 || s.e > s.m) return MEMO_EC_EINVAL;
     if (s.e == 0 || s.n == 0) continue;
     if (s.S == 0 || s.S % 64 || !s.surv_idx || !s.surv || !s.lost_idx || !s.out) return MEMO_EC_EINVAL;
-    if (s.S >= kMaxShard) return MEMO_EC_ERANGE;
+    if (s.S >= kMaxShard || too_big(s.n, (size_t)(s.k + s.e) * s.S + s.k + s.e)) return MEMO_EC_ERANGE;
     RPiece p;
     p.seg = i;
     p.k = s.k;
@@ -1179,7 +1188,7 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
   if (int rc = check_km(k, m)) return rc;
   if (m == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !data || !parity) return MEMO_EC_EINVAL;
-  if (S >= kMaxShard) return MEMO_EC_ERANGE;
+  if (S >= kMaxShard || too_big(n, (size_t)(k + m) * S)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   if (where == MEMO_EC_DEVICE) return encode_device(c, k, m, S, n, data, parity, c->stream);
   if (where != MEMO_EC_HOST && where != MEMO_EC_HOST_PINNED) return MEMO_EC_EINVAL;
@@ -1210,7 +1219,7 @@ int memo_ec_rebuild_uniform(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e < 0 || e > m) return MEMO_EC_EINVAL;
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
-  if (S >= kMaxShard) return MEMO_EC_ERANGE;
+  if (S >= kMaxShard || too_big(n, (size_t)(k + e) * S + k + e)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   const int R = mac_rbound(e), KC = mac_kchunk(k, R);
   const uint32_t* tab = nullptr;
@@ -1239,6 +1248,7 @@ int memo_ec_decode_rows(memo_ec_ctx* c, int k, int m, size_t n, const uint8_t* s
   if (e < 0 || e > m) return MEMO_EC_EINVAL;
   if (n == 0 || e == 0) return MEMO_EC_OK;
   if (!surv_idx || !lost_idx || !rows) return MEMO_EC_EINVAL;
+  if (too_big(n, (size_t)e * k + k + e)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   const uint32_t* lw0 = nullptr;
   if (int rc = lw0_table(c, k, m, &lw0)) return rc;
@@ -1255,7 +1265,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   if (e < 0 || e > m) return MEMO_EC_EINVAL;
   if (e == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !surv_idx || !surv || !lost_idx || !out) return MEMO_EC_EINVAL;
-  if (S >= kMaxShard) return MEMO_EC_ERANGE;
+  if (S >= kMaxShard || too_big(n, (size_t)(k + e) * S + k + e)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   const bool fused = rebuild_fused(c, n * (size_t)k * S);
   if (where == MEMO_EC_DEVICE) {
@@ -1382,6 +1392,7 @@ int memo_ec_encode_segments(memo_ec_ctx* c, int nseg, const memo_ec_segment* seg
       return MEMO_EC_EINVAL;
     if (segs[i].S >= kMaxShard) return MEMO_EC_ERANGE;
     if (segs[i].n > max_blocks_per_launch(c, segs[i].S)) return MEMO_EC_ERANGE;
+    if (too_big(segs[i].n, (size_t)(segs[i].k + segs[i].m) * segs[i].S)) return MEMO_EC_ERANGE;
     const int kc = mac_kchunk(segs[i].k, mac_rbound(segs[i].m));
     size_t ci = 0;
     while (ci < classes.size() && classes[ci] != kc) ++ci;
@@ -1619,6 +1630,7 @@ int memo_ec_sha256_batch(memo_ec_ctx* c, size_t n, const uint8_t* prefix, size_t
 int memo_ec_fill_blocks(memo_ec_ctx* c, uint64_t seed, uint64_t first_block, size_t n, size_t B,
                         int k, size_t S, uint8_t* out) {
   if (!c || k < 1 || S % 16 || (size_t)k * S < B || (n && !out)) return MEMO_EC_EINVAL;
+  if (S >= kMaxShard || too_big(n, (size_t)k * S)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   FillArgs a{out, seed, first_block, n, B, (uint64_t)k * S};
   return hip_rc(launch_fill(a, c->stream));
@@ -1628,6 +1640,7 @@ int memo_ec_gather_shards(memo_ec_ctx* c, int k, int m, size_t S, size_t n, cons
                           const uint8_t* parity, const uint8_t* idx, int cnt, uint8_t* out) {
   if (!c || check_km(k, m) || S % 16 || cnt < 0 || (n && cnt && (!data || !idx || !out)))
     return MEMO_EC_EINVAL;
+  if (S >= kMaxShard || too_big(n, (size_t)cnt * S + cnt)) return MEMO_EC_ERANGE;
   DeviceGuard g(c->device);
   GatherArgs a{data, parity, idx, out, S, n, (uint32_t)k, (uint32_t)m, (uint32_t)cnt};
   return hip_rc(launch_gather(a, c->stream));

@@ -500,6 +500,40 @@ def test_noops_and_argument_errors(codec):
     codec.synchronize()
 
 
+def test_call_size_overflow_refused(codec):
+    """Block counts whose byte products overflow, or pass 2^50 bytes, are
+    refused with ERANGE before any scratch or grid is sized from them and
+    before anything is launched (the ctx stays usable).  Each call's n is
+    taken just past 2^50 bytes, past 2^64 (a wrapping product), and 2^62."""
+    import ctypes
+    from memo_amd import ec
+    L = ec._lib()
+    d = empty(1, 16 * 64)
+    p = d.data_ptr()
+    cx = codec._ctx
+
+    def ns(per):
+        return [(1 << 50) // per + 1, (1 << 64) // per + 1, 1 << 62]
+
+    for n in ns(14 * 64):
+        assert L.memo_ec_encode_batch(cx, 10, 4, 64, n, p, p, 2) == -6, n
+    for n in ns(14 * 64 + 14):
+        assert L.memo_ec_rebuild_batch(cx, 10, 4, 64, n, p, p, p, 4, p, 2) == -6, n
+        assert L.memo_ec_rebuild_uniform(cx, 10, 4, 64, n, p, p, p, 4, p, 2) == -6, n
+        seg = ec.RebuildSegment(k=10, m=4, S=64, n=n, surv_idx=p, surv=p, lost_idx=p, e=4,
+                                uniform=0, out=p)
+        assert L.memo_ec_rebuild_segments(cx, 1, ctypes.byref(seg), 2) == -6, n
+    for n in ns(4 * 10 + 14):
+        assert L.memo_ec_decode_rows(cx, 10, 4, n, p, p, 4, p) == -6, n
+    for n in ns(10 * 64):
+        assert L.memo_ec_fill_blocks(cx, 1, 0, n, 64, 10, 64, p) == -6, n
+    for n in ns(4 * 64 + 4):
+        assert L.memo_ec_gather_shards(cx, 10, 4, 64, n, p, p, p, 4, p) == -6, n
+    codec.synchronize()
+    assert L.memo_ec_encode_batch(cx, 10, 4, 64, 1, p, p, 2) == 0
+    codec.synchronize()
+
+
 def test_full_size_c2_c3_round_trip(codec, O, rebuild_path):
     """BASELINE.json C2/C3 at full size (4096 x 1 MiB, RS(10,4), e=4), the
     WHOLE batch against the CPU oracle: all 4096 blocks' data and parity
