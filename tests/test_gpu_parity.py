@@ -574,6 +574,50 @@ def test_full_size_c2_c3_round_trip(codec, O, rebuild_path):
     assert torch.equal(out2, p)
 
 
+@pytest.mark.parametrize("k,m,B,n", [(10, 4, 1 << 20, 4096), (16, 4, 4096, 1 << 20)])
+def test_full_size_linearity(codec, k, m, B, n, rebuild_path):
+    """Size-independent properties of the code at full headline size (C2 /
+    C3's 4096 x 1 MiB RS(10,4) and the 1M x 4 KiB RS(16,4) batch), over the
+    whole batch: encode and rebuild are GF(2)-linear, enc(a ^ b) = enc(a) ^
+    enc(b) and rebuild(a ^ b) = rebuild(a) ^ rebuild(b) with the same
+    erasure patterns; zero data encodes and rebuilds to zero."""
+    import torch
+    S = _shard_size(B, k)
+    e = m
+    a, b = fill(codec, 0, n, B, k, S), fill(codec, n, n, B, k, S)
+    pa, pb, pab = empty(n, m * S), empty(n, m * S), empty(n, m * S)
+    codec.encode(k, m, a, pa)
+    codec.encode(k, m, b, pb)
+    codec.synchronize()  # the codec's stream is not torch's: order by hand
+    ab = torch.bitwise_xor(a, b)
+    torch.cuda.synchronize()
+    codec.encode(k, m, ab, pab)
+    codec.synchronize()
+    assert torch.equal(pab, torch.bitwise_xor(pa, pb))
+    s, l = ec_erasures(n, k, m, e)
+    sd, ld = dev(s), dev(l)
+    ra, rb, rab = empty(n, e * S), empty(n, e * S), empty(n, e * S)
+    surv = empty(n, k * S)
+    for d, p, r in [(a, pa, ra), (b, pb, rb), (ab, pab, rab)]:
+        codec.gather_shards(k, m, S, n, d, p, sd, surv)
+        codec.rebuild(k, m, sd, surv, ld, r)
+    codec.synchronize()
+    assert torch.equal(rab, torch.bitwise_xor(ra, rb))
+    del b, pb, rb, ab, pab, rab
+    a.zero_()
+    torch.cuda.synchronize()
+    codec.encode(k, m, a, pa)
+    codec.gather_shards(k, m, S, n, a, pa, sd, surv)
+    codec.rebuild(k, m, sd, surv, ld, ra)
+    codec.synchronize()
+    assert not pa.any() and not ra.any()
+
+
+def _shard_size(B, k):
+    from memo_amd import ec
+    return ec.shard_size(B, k)
+
+
 @pytest.mark.parametrize("k,m", [(16, 4), (10, 4)])
 def test_full_size_small_block_rebuild(codec, O, k, m):
     """bench.py's rebuild_small batches at full size: 1,048,576 x 4 KiB
