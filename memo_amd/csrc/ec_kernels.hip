@@ -1925,6 +1925,22 @@ hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
   std::vector<DecodePick> picks;
   for (int i = 0; i < na; ++i)
     if (as[i].n) picks.push_back(decode_pick(as[i]));
+  // A segment small enough for the column-per-lane kernel rides in the
+  // exact-k launch of another segment with the same k and m bound, instead
+  // of taking a launch of its own (a mixed rebuild's 64 KiB-4 MiB groups
+  // beside its 4 KiB group of the same code).
+  for (auto& p : picks) {
+    if (p.kind != 0) continue;
+    DecodeArgs a = p.a;
+    a.wide_max = 0;
+    const DecodePick r = decode_pick(a);
+    if (r.kind != 1) continue;
+    for (const auto& q : picks)
+      if (q.kind == 1 && q.param == r.param) {
+        p = r;
+        break;
+      }
+  }
   std::vector<bool> done(picks.size(), false);
   for (size_t i = 0; i < picks.size(); ++i) {
     if (done[i]) continue;

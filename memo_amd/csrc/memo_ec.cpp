@@ -1068,7 +1068,7 @@ const char* memo_ec_strerror(int code) {
     case MEMO_EC_EHIP: return "HIP runtime error";
     case MEMO_EC_ESINGULAR: return "survivor shards cannot rebuild the block";
     case MEMO_EC_ENODEV: return "no such GPU";
-    case MEMO_EC_ERANGE: return "k or m beyond this build's limits";
+    case MEMO_EC_ERANGE: return "k, m, shard or call size beyond this build's limits";
     default: return "unknown error";
   }
 }

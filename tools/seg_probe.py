@@ -11,6 +11,9 @@ import torch
 sys.path.insert(0, ".")
 from memo_amd import ec  # noqa: E402
 
+if len(sys.argv) > 3:  # another build of the library (an A/B's other side)
+    ec.LIB_PATH = sys.argv[3]
+
 SEED = 0x6D656D6F
 
 
