@@ -20,6 +20,8 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     from memo_amd import ec
+    if os.environ.get("MEMO_EC_PROBE_LIB"):  # another build of the library (an A/B's other side)
+        ec.LIB_PATH = os.environ["MEMO_EC_PROBE_LIB"]
     k, m, B, n = (int(x) for x in sys.argv[1:5])
     e = int(sys.argv[5]) if len(sys.argv) > 5 else m
     launches = int(sys.argv[6]) if len(sys.argv) > 6 else 20
