@@ -1321,9 +1321,12 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   }
   size_t nb = std::max<size_t>(1, c->opt.pipe_bytes / in_b);
   nb = std::min(nb, n);
-  // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e]
+  // slot layout: [surv nb*in_b | out nb*out_b | surv_idx nb*k | lost_idx nb*e];
+  // pinned callers' data moves by DMA from their own buffers, so their host
+  // slot holds the indices only (no pinned bounce buffers of the batch size)
   const size_t slot = nb * (in_b + out_b + idx_b);
-  if (int rc = ensure_slots(c, slot, slot)) return rc;
+  const size_t hshift = pinned ? nb * (in_b + out_b) : 0;  // host slot offset of the device layout
+  if (int rc = ensure_slots(c, slot, slot - hshift)) return rc;
   const size_t tabs = tab_bytes(k, e, nb, fused);
   if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
@@ -1332,9 +1335,9 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
       [&](int s, size_t b0, size_t cnt, hipStream_t st) -> int {
         uint8_t* h = c->h_slot[s];
         uint8_t* d = c->d_slot[s];
-        std::memcpy(h + o_sidx, surv_idx + b0 * k, cnt * k);  // indices: always bounced
-        std::memcpy(h + o_lidx, lost_idx + b0 * e, cnt * e);
-        HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx, nb * idx_b, hipMemcpyHostToDevice, st));
+        std::memcpy(h + o_sidx - hshift, surv_idx + b0 * k, cnt * k);  // indices: always bounced
+        std::memcpy(h + o_lidx - hshift, lost_idx + b0 * e, cnt * e);
+        HIPCHK(hipMemcpyAsync(d + o_sidx, h + o_sidx - hshift, nb * idx_b, hipMemcpyHostToDevice, st));
         const uint8_t* src = surv + b0 * in_b;
         if (!pinned) {
           par_memcpy(c, h, src, cnt * in_b);
@@ -1528,12 +1531,14 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
     }
     return dp;
   };
-  auto stage_idx = [&](const Wave& w, uint8_t* h) {
+  // indices staged at their slot offsets less `shift` (pinned pipeline
+  // calls keep only the indices in their host slot)
+  auto stage_idx = [&](const Wave& w, uint8_t* h, size_t shift = 0) {
     for (size_t i : w.ids) {
       const RPiece& p = ch[i].p;
       if (p.mode == MAC_ENCODE) continue;
-      std::memcpy(h + ch[i].o_idx, p.sidx, p.n * (size_t)p.k);
-      std::memcpy(h + ch[i].o_idx + p.n * (size_t)p.k, p.lidx, p.n * (size_t)p.e);
+      std::memcpy(h + ch[i].o_idx - shift, p.sidx, p.n * (size_t)p.k);
+      std::memcpy(h + ch[i].o_idx - shift + p.n * (size_t)p.k, p.lidx, p.n * (size_t)p.e);
     }
   };
   if (zc) {
@@ -1560,7 +1565,14 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
     if (drc == MEMO_EC_OK && (__atomic_load_n(h_st, __ATOMIC_ACQUIRE) & 1u)) drc = MEMO_EC_ESINGULAR;
     return drc;
   }
-  if (int rc = ensure_slots(c, slot, slot)) return rc;
+  // pinned: the survivors and outputs move by DMA from the caller's
+  // buffers, and the host slot holds a wave's indices only
+  size_t hslot = slot;
+  if (pinned) {
+    hslot = 64;
+    for (const Wave& w : waves) hslot = std::max(hslot, w.idx);
+  }
+  if (int rc = ensure_slots(c, slot, hslot)) return rc;
   if (int rc = ensure_tabs(c, kSlots * rows)) return rc;
   const int rc = run_waves(
       c, waves.size(),
@@ -1568,8 +1580,10 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
         const Wave& w = waves[wi];
         uint8_t* h = c->h_slot[s];
         uint8_t* d = c->d_slot[s];
-        stage_idx(w, h);
-        if (w.idx) HIPCHK(hipMemcpyAsync(d + w.in + w.out, h + w.in + w.out, w.idx, hipMemcpyHostToDevice, st));
+        const size_t shift = pinned ? w.in + w.out : 0;
+        stage_idx(w, h, shift);
+        if (w.idx)
+          HIPCHK(hipMemcpyAsync(d + w.in + w.out, h + w.in + w.out - shift, w.idx, hipMemcpyHostToDevice, st));
         for (size_t i : w.ids) {
           if (pinned) {
             HIPCHK(hipMemcpyAsync(d + ch[i].o_in, ch[i].p.surv, ch[i].in, hipMemcpyHostToDevice, st));
