@@ -717,8 +717,19 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist_mod
-        # gloo on the host: the barrier and the max/gather of timings only
-        dist_mod.init_process_group("gloo")
+        # gloo on the host: the barrier and the max/gather of timings only.
+        # Its connect messages ("[Gloo] Rank r is connected to ...") are
+        # written to stdout; stdout carries only rank 0's JSON line, so they
+        # go to stderr.
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist_mod.init_process_group("gloo")
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         dist = dist_mod
     if torch.cuda.device_count() <= local:
         raise SystemExit("bench.py: rank %d needs cuda:%d, %d visible" % (rank, local,

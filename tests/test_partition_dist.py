@@ -166,8 +166,10 @@ def test_cpu_share_is_bounded():
 def _bench_json(r):
     import json
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    assert len(lines) == 1, r.stdout
+    # stdout is exactly rank 0's JSON line (gloo's connect messages go to
+    # stderr), as the driver reads it
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), r.stdout
     return json.loads(lines[0])
 
 
