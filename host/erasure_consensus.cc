@@ -259,6 +259,7 @@ PinnedArena::~PinnedArena() {
 }
 
 PinnedArena::Lease PinnedArena::lease(size_t bytes) {
+  ++leases_;
   bytes = std::max<size_t>(bytes, 64);
   {
     std::lock_guard<std::mutex> g(mu_);

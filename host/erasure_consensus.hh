@@ -20,6 +20,7 @@
 #pragma once
 
 #include <chrono>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -120,8 +121,12 @@ class PinnedArena {
   PinnedArena(const PinnedArena&) = delete;
   PinnedArena& operator=(const PinnedArena&) = delete;
   Lease lease(size_t bytes);
+  // leases handed out so far (tests: a multi-fetch or repair chunk takes
+  // one survivor and one output lease, however many batches it has)
+  uint64_t leases() const { return leases_.load(); }
 
  private:
+  std::atomic<uint64_t> leases_{0};
   struct Buf {
     uint8_t* p;
     size_t cap;
@@ -303,6 +308,7 @@ class ErasureConsensus : public StackedConsensus {
   // Store many immutable blocks with one encode call per batch.
   void store_many(const std::vector<Block>& blocks);
   const Codec& codec() const { return codec_; }
+  uint64_t arena_leases() const { return arena_.leases(); }
   const ErasureOptions& options() const { return o_; }
 
  protected:

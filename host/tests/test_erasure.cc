@@ -433,6 +433,7 @@ TEST(multi_fetch_batches_decodes, true) {
   req.push_back(mut.address);
   const uint64_t calls0 = net.ec->codec().rebuild_calls() + net.ec->codec().uniform_calls();
   const uint64_t seg0 = net.ec->codec().segments_calls();
+  const uint64_t leases0 = net.ec->arena_leases();
   std::vector<Address> seen;
   int ok = 0, missing_seen = 0;
   net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr e) {
@@ -470,6 +471,10 @@ TEST(multi_fetch_batches_decodes, true) {
   const uint64_t batch_calls = net.ec->codec().segments_calls() - seg0;
   CHECK(net.ec->codec().rebuild_calls() + net.ec->codec().uniform_calls() == calls0);
   CHECK(batch_calls == 1);
+  // one survivor and one output lease for all the batches of the call (a
+  // lease per batch cost a pinned allocation each: 7x slower 4 KiB
+  // degraded fetches, profiles/r03_bench_plugin_4k.json)
+  CHECK(net.ec->arena_leases() - leases0 == 2);
   size_t need_decode = 0;
   for (auto& b : blocks) {
     const uint64_t c = net.ec->codec().rebuild_calls();
@@ -969,9 +974,11 @@ TEST(evict_one_node_uses_uniform_rebuild, true) {
     if (!victim || net.ec->node_blocks(n->id) > net.ec->node_blocks(victim->id)) victim = n;
   const size_t held = net.ec->node_blocks(victim->id);
   const uint64_t u0 = net.ec->codec().uniform_segments();
+  const uint64_t leases0 = net.ec->arena_leases();
   victim->up = false;
   auto rep = net.ec->evict(victim->id);
   CHECK(rep.blocks_repaired == held && rep.unrecoverable == 0);
+  CHECK(net.ec->arena_leases() - leases0 == 2);  // one lease pair per repair chunk
   const uint64_t uniform = net.ec->codec().uniform_segments() - u0;
   std::printf("  (%zu blocks repaired in %zu codec calls, %llu shared-pattern segments)\n", held,
               rep.codec_calls, (unsigned long long)uniform);
