@@ -78,6 +78,12 @@ def parse(argv=None):
     ap.add_argument("--sweep-gib", type=float, default=4.0, help="payload GiB per sweep point")
     ap.add_argument("--same-device", action="store_true",
                     help="every rank on cuda:0 (rehearse N>1 on a 1-GPU box)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the whole-batch oracle comparisons after the timed steps")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 mixed-geometry point")
+    ap.add_argument("--c5-gib", type=float, default=4.0, help="payload GiB of the C5 mixed point")
+    ap.add_argument("--rank-timeout", type=float, default=600.0,
+                    help="seconds a rank may take (launcher kill bound, gloo collective timeout)")
     return ap.parse_args(argv)
 
 
@@ -139,9 +145,7 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
     ~gib GiB of payload per point.  Each point times one encode launch and
     one rebuild of the same blocks with e = m random erasures per block (the
     metric is encode+rebuild), both checked bit-exact on the GPU.  Then the
-    same 12 smaller groups as ONE memo_ec_encode_segments call and ONE
-    memo_ec_rebuild_segments call (one launch per shard-chunk class, back to
-    back; timed from before the first launch to after the last)."""
+    12-group mixed calls of c5_mixed."""
     def frac(alg, ms):
         return round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
 
@@ -174,7 +178,7 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             pt = {"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
                   "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
                   "frac": frac((k + m) * S * n, ms),
-                  "rebuild": {"erasures": e, "kernel": ec.rebuild_path(n, k, S), "step_ms": round(rs, 4),
+                  "rebuild": {"erasures": e, "kernel": codec.rebuild_path(n, k, S), "step_ms": round(rs, 4),
                               "GiBs": round(n * B / (rs * 1e-3) / 2**30, 1),
                               "frac": frac((k + e) * S * n, rs),
                               "bit_exact": bool(torch.equal(out, want))},
@@ -206,33 +210,7 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             points.append(pt)
             log("sweep RS(%d,%d) %d B: encode %.3f, rebuild %.3f" % (k, m, B, pt["frac"], pt["rebuild"]["frac"]))
             del d, p, surv, want, out, sd, ld
-    segs, rsegs, checks, alg, ralg, pay = [], [], [], 0, 0, 0
-    for gi, (k, m) in enumerate([(4, 2), (10, 4), (16, 4)]):
-        for B in [4 << 10, 64 << 10, 1 << 20, 4 << 20]:
-            S = ec.shard_size(B, k)
-            n = max(1, int(gib * 2**30 / 12) // B)
-            d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
-            p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
-            codec.fill_blocks(SEED, 0, n, B, k, S, d)
-            codec.encode(k, m, d, p)
-            e, _, _, sd, ld, surv, want, out = rebuild_inputs(k, m, S, n, d, p, fb=gi)
-            segs.append((k, m, S, n, d, p))
-            rsegs.append(dict(k=k, m=m, surv_idx=sd, surv=surv, lost_idx=ld, out=out))
-            checks.append((out, want))
-            alg += (k + m) * S * n
-            ralg += (k + e) * S * n
-            pay += n * B
-    _, (kms, rms), _ = timed_steps(torch, [lambda: codec.encode_segments(segs),
-                                           lambda: codec.rebuild_segments(rsegs)],
-                                   steps, warmup, settle_ms, None, stream)
-    codec.synchronize()
-    ms, rs = float(np.mean(kms)), float(np.mean(rms))
-    fused = {"segments": len(segs), "kernel_ms": round(ms, 4),
-             "GiBs": round(pay / (ms * 1e-3) / 2**30, 1), "frac": frac(alg, ms),
-             "rebuild": {"step_ms": round(rs, 4), "GiBs": round(pay / (rs * 1e-3) / 2**30, 1),
-                         "frac": frac(ralg, rs),
-                         "bit_exact": all(bool(torch.equal(o, w)) for o, w in checks)},
-             "encode_rebuild_GiBs": round(2 * pay / ((ms + rs) * 1e-3) / 2**30, 1)}
+    fused = c5_mixed(torch, ec, codec, stream, gib, steps, warmup, settle_ms)
     return {"workload": "BASELINE.json C5: RS(k,m) encode and rebuild (e = m random erasures per "
                         "block) per (k,m) x block size, ~%.1f GiB payload per point; fused = 12 "
                         "mixed groups in one encode_segments call and one rebuild_segments call "
@@ -240,12 +218,16 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             "points": points, "fused": fused}
 
 
-def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
+def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms, stage=None, threads=1):
     """Small-block rebuild: 4 KiB blocks (~4 GiB of payload), 4 random
     erasures per block, so every block has its own decode rows and a
     256-column tile spans up to 17 blocks.  Encode of the same blocks is
     timed beside it (same process, same clocks), and so is the repair case
-    of one pattern for every block (memo_ec_rebuild_uniform)."""
+    of one pattern for every block (memo_ec_rebuild_uniform).  The memory
+    system's rate for the same traffic (memo_ec_stream_probe) is the
+    achievable denominator.  With a HostStage, the whole per-block-pattern
+    batch is compared with the CPU oracle's rebuild, and the uniform one
+    with the original shards."""
     res = {}
     for (k, m) in [(10, 4), (16, 4)]:
         B, n, e = 4096, 1 << 20, 4
@@ -268,6 +250,18 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
         ms = float(np.mean(rkms))
         alg = (k + e) * S * n
         ok = bool(torch.equal(out, want))
+        probe = probe_rate(torch, codec, stream, k, e, surv, want)
+        codec.gather_shards(k, m, S, n, d, p, ld, want)  # the probe overwrote it
+        row = {"blocks": n, "block_bytes": B, "shard_bytes": S, "erasures": e,
+               "kernel": codec.rebuild_kernel_name(n, k, S),
+               "step_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
+               "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+               "encode_frac_same_blocks": round((k + m) * S * n / (float(np.mean(ekms)) * 1e-3) / 1e9
+                                                / PEAK_HBM_GBS, 4),
+               "achievable": probe, "frac_of_achievable": round(probe["kernel_ms_avg"] / ms, 4),
+               "bit_exact": ok}
+        if stage is not None:
+            row["oracle"] = verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, threads)
         # the repair case: one lost node, every block the same pattern
         # (memo_ec_rebuild_uniform), here block 0's
         su, lu = s_idx[0], l_idx[0]
@@ -279,18 +273,197 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms):
                                     steps, warmup, settle_ms, None, stream)
         codec.synchronize()
         ums = float(np.mean(ukms))
-        res["RS(%d,%d)" % (k, m)] = {
-            "blocks": n, "block_bytes": B, "shard_bytes": S, "erasures": e,
-            "step_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
-            "frac": round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-            "encode_frac_same_blocks": round((k + m) * S * n / (float(np.mean(ekms)) * 1e-3) / 1e9
-                                             / PEAK_HBM_GBS, 4),
-            "bit_exact": ok,
-            "uniform_pattern": {"step_ms": round(ums, 4),
-                                "frac": round(alg / (ums * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
-                                "bit_exact": bool(torch.equal(out, want))}}
+        row["uniform_pattern"] = {"step_ms": round(ums, 4),
+                                  "frac": round(alg / (ums * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+                                  "bit_exact": bool(torch.equal(out, want)),
+                                  "check": "every rebuilt shard == the original shard it replaces"}
+        res["RS(%d,%d)" % (k, m)] = row
+        log("rebuild_small RS(%d,%d): %.3f of peak, %.3f of achievable" % (
+            k, m, row["frac"], row["frac_of_achievable"]))
         del d, p, surv, out, want, sd, ld, sdu, ldu
     return res
+
+
+C5_CODES = [(4, 2), (10, 4), (16, 4)]
+C5_SIZES = [4 << 10, 64 << 10, 1 << 20, 4 << 20]
+
+
+def c5_mixed(torch, ec, codec, stream, gib, steps, warmup, settle_ms, stage=None, threads=1):
+    """BASELINE.json C5 as the plugin issues it: 12 groups, (k,m) in
+    {(4,2),(10,4),(16,4)} x B in {4 KiB, 64 KiB, 1 MiB, 4 MiB}, ~gib GiB of
+    payload in all, encoded by ONE memo_ec_encode_segments call and rebuilt
+    (e = m random erasures per block) by ONE memo_ec_rebuild_segments call --
+    the shape of a multi-address fetch, which hands a whole mixed batch to one
+    call (Consensus::_fetch(vector<AddressVersion>), src/memo/model/doughnut/
+    Consensus.cc:101-124; Paxos::_fetch, consensus/Paxos.cc:1857-1890).  One
+    launch per code class, back to back; timed from before the first launch
+    to after the last.  With a HostStage every group's parity and rebuilt
+    shards are compared with the CPU oracle, and the rebuilt shards with the
+    original ones."""
+    def frac(alg, ms):
+        return round(alg / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)
+
+    groups, segs, rsegs, alg, ralg, pay = [], [], [], 0, 0, 0
+    for gi, (k, m) in enumerate(C5_CODES):
+        for B in C5_SIZES:
+            S = ec.shard_size(B, k)
+            n = max(1, int(gib * 2**30 / (len(C5_CODES) * len(C5_SIZES))) // B)
+            e = m
+            d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+            p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
+            codec.fill_blocks(SEED, 0, n, B, k, S, d)
+            s_idx, l_idx = ec.erasures(SEED, gi, n, k, m, e)
+            sd, ld = torch.from_numpy(s_idx).cuda(), torch.from_numpy(l_idx).cuda()
+            surv = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
+            want = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+            out = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
+            groups.append(dict(k=k, m=m, B=B, S=S, n=n, e=e, d=d, p=p, s_idx=s_idx, l_idx=l_idx,
+                               sd=sd, ld=ld, surv=surv, want=want, out=out))
+            segs.append((k, m, S, n, d, p))
+            rsegs.append(dict(k=k, m=m, surv_idx=sd, surv=surv, lost_idx=ld, out=out))
+            alg += (k + m) * S * n
+            ralg += (k + e) * S * n
+            pay += n * B
+    # parity by the mixed call itself, then the survivors / lost shards of it
+    codec.encode_segments(segs)
+    for g in groups:
+        codec.gather_shards(g["k"], g["m"], g["S"], g["n"], g["d"], g["p"], g["sd"], g["surv"])
+        codec.gather_shards(g["k"], g["m"], g["S"], g["n"], g["d"], g["p"], g["ld"], g["want"])
+    _, (kms, rms), _ = timed_steps(torch, [lambda: codec.encode_segments(segs),
+                                           lambda: codec.rebuild_segments(rsegs)],
+                                   steps, warmup, settle_ms, None, stream)
+    codec.synchronize()
+    ms, rs = float(np.mean(kms)), float(np.mean(rms))
+    res = {"workload": "BASELINE.json C5: 12 groups (k,m) in {(4,2),(10,4),(16,4)} x B in {4 KiB, "
+                       "64 KiB, 1 MiB, 4 MiB}, %.1f GiB payload; one encode_segments call and one "
+                       "rebuild_segments call (e = m random erasures per block) per step" % (pay / 2**30),
+           "segments": len(segs), "payload_bytes": pay,
+           "encode": {"kernel_ms": round(ms, 4), "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
+                      "frac": frac(alg, ms), "bytes_per_call": alg},
+           "rebuild": {"step_ms": round(rs, 4), "GiBs": round(pay / (rs * 1e-3) / 2**30, 1),
+                       "frac": frac(ralg, rs), "bytes_per_call": ralg},
+           "encode_rebuild_GiBs": round(2 * pay / ((ms + rs) * 1e-3) / 2**30, 1)}
+    per = []
+    for g in groups:
+        x = {"k": g["k"], "m": g["m"], "block_bytes": g["B"], "blocks": g["n"],
+             "round_trip_bit_exact": bool(torch.equal(g["out"], g["want"]))}
+        if stage is not None:
+            ve = verify_encode(stage, g["k"], g["m"], g["S"], g["d"], g["p"], threads)
+            vr = verify_rebuild(stage, g["k"], g["m"], g["S"], g["s_idx"], g["surv"], g["l_idx"],
+                                g["out"], threads)
+            x["oracle_encode_bit_exact"] = ve["bit_exact"]
+            x["oracle_rebuild_bit_exact"] = vr["bit_exact"]
+        per.append(x)
+    res["groups"] = per
+    res["round_trip_bit_exact"] = all(x["round_trip_bit_exact"] for x in per)
+    if stage is not None:
+        res["oracle_bit_exact"] = all(x["oracle_encode_bit_exact"] and x["oracle_rebuild_bit_exact"]
+                                      for x in per)
+    log("c5 mixed: encode %.3f, rebuild %.3f of peak" % (res["encode"]["frac"], res["rebuild"]["frac"]))
+    return res
+
+
+class HostStage:
+    """Page-locked host staging for the whole-batch oracle comparisons:
+    device rows are copied chunk by chunk (one DMA each, ~chunk_bytes per
+    buffer) into reused pinned buffers, the CPU oracle runs on them, and no
+    batch is ever held whole in host memory (an 8-rank node checks 8
+    batches at once)."""
+
+    def __init__(self, torch, chunk_bytes=256 << 20):
+        self.torch = torch
+        self.chunk = chunk_bytes
+        self.pinned = {}
+        self.plain = {}
+
+    def rows_per_chunk(self, row_bytes):
+        return max(1, self.chunk // row_bytes)
+
+    def fetch(self, name, dev, r0, r1):
+        """numpy view of rows [r0, r1) of a 2-D uint8 device tensor."""
+        t = self.torch
+        cols = dev.shape[1]
+        nb = (r1 - r0) * cols
+        b = self.pinned.get(name)
+        if b is None or b.numel() < nb:
+            b = t.empty(max(nb, self.chunk), dtype=t.uint8, pin_memory=True)
+            self.pinned[name] = b
+        v = b[:nb].view(r1 - r0, cols)
+        v.copy_(dev[r0:r1])
+        return v.numpy()
+
+    def scratch(self, name, rows, cols):
+        """64-byte-aligned host rows (the oracle's output)."""
+        from oracle import oracle as O
+        nb = rows * cols
+        b = self.plain.get(name)
+        if b is None or b.size < nb:
+            b = O.aligned_empty((max(nb, self.chunk),))
+            self.plain[name] = b
+        return b[:nb].reshape(rows, cols)
+
+
+def same_bytes(a, b):
+    """a == b over two equal-shape uint8 arrays, in 64 MiB slices (no
+    full-size boolean temporary)."""
+    if a.shape != b.shape:
+        return False
+    x, y = a.reshape(-1), b.reshape(-1)
+    step = 64 << 20
+    return all(np.array_equal(x[i:i + step], y[i:i + step]) for i in range(0, x.size, step))
+
+
+def verify_encode(stage, k, m, S, d, p, threads):
+    """Every parity byte of a device batch against the CPU oracle
+    (oracle/rs_simd.c, itself checked against the scalar oracle and the
+    golden fixtures by tests/test_oracle.py) run on the same data bytes."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    n = d.shape[0]
+    step = stage.rows_per_chunk((k + m) * S)
+    ok = True
+    for r0 in range(0, n, step):
+        r1 = min(n, r0 + step)
+        hd = stage.fetch("in", d, r0, r1)
+        hp = stage.fetch("out", p, r0, r1)
+        want = stage.scratch("want", r1 - r0, m * S)
+        O.encode_simd(k, m, S, hd, threads=threads, out=want)
+        ok = ok and same_bytes(want, hp)
+    return {"blocks": n, "bytes_compared": n * m * S, "bit_exact": ok,
+            "seconds": round(time.perf_counter() - t0, 2)}
+
+
+def verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, threads):
+    """Every rebuilt byte of a device batch against the CPU oracle's rebuild
+    (per-block Gauss-Jordan decode rows + the vectorised MAC) of the same
+    survivor bytes and erasure patterns."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    n, e = l_idx.shape
+    step = stage.rows_per_chunk((k + e) * S)
+    ok = True
+    for r0 in range(0, n, step):
+        r1 = min(n, r0 + step)
+        hs = stage.fetch("in", surv, r0, r1)
+        ho = stage.fetch("out", out, r0, r1)
+        want = stage.scratch("want", r1 - r0, e * S)
+        O.rebuild_simd(k, m, S, s_idx[r0:r1], hs, l_idx[r0:r1], threads=threads, out=want)
+        ok = ok and same_bytes(want, ho)
+    return {"blocks": n, "erasures": e, "bytes_compared": n * e * S, "bit_exact": ok,
+            "seconds": round(time.perf_counter() - t0, 2)}
+
+
+def probe_rate(torch, codec, stream, kin, r, inp, out, launches=10, warmup=5):
+    """Achievable rate of the MAC's own traffic on this GPU: memo_ec_stream_probe
+    (the same tiles and 16-byte non-temporal loads / stores, XOR in place of
+    the GF arithmetic) over the same buffers, HIP events on `stream`."""
+    n, S = inp.shape[0], inp.shape[1] // kin
+    _, (pms,), _ = timed_steps(torch, [lambda: codec.stream_probe(kin, r, inp, out)], launches,
+                               warmup, 0, None, stream)
+    ms = float(np.mean(pms))
+    return {"kernel": "stream_probe_kernel (the MAC's loads/stores, XOR only)",
+            "GBs": round((kin + r) * S * n / (ms * 1e-3) / 1e9, 1), "kernel_ms_avg": round(ms, 4),
+            "frac": round((kin + r) * S * n / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
 
 
 def _rate(fn, nbytes, seconds):
@@ -312,54 +485,83 @@ def host_cores():
         return os.cpu_count() or 1
 
 
-def cpu_share():
-    """CPUs this process may actually keep busy: the affinity set, capped by
-    the cgroup CPU quota and by OMP_NUM_THREADS when set (the GPU box gives a
-    one-GPU job 16 CPUs of a 256-CPU machine; `nproc` reports 16 there)."""
-    n = host_cores()
+def _cgroup_cpus():
+    """The cgroup CPU quota of this process (None: no quota)."""
     try:
         with open("/sys/fs/cgroup/cpu.max") as f:
             q, per = f.read().split()[:2]
-        if q != "max":
-            n = min(n, max(1, int(int(q) // int(per))))
+        return None if q == "max" else max(1, int(int(q) // int(per)))
     except (OSError, ValueError):
         try:
             with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
                 q = int(f.read())
             with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
                 per = int(f.read())
-            if q > 0:
-                n = min(n, max(1, q // per))
+            return max(1, q // per) if q > 0 else None
         except (OSError, ValueError):
-            pass
+            return None
+
+
+def _omp_threads():
     try:
-        omp = int(os.environ.get("OMP_NUM_THREADS", "0"))
-        if omp > 0:
-            n = min(n, omp)
+        return max(0, int(os.environ.get("OMP_NUM_THREADS", "0")))
     except ValueError:
-        pass
+        return 0
+
+
+def cpu_share():
+    """CPUs this process may actually keep busy: the affinity set, capped by
+    the cgroup CPU quota and by OMP_NUM_THREADS when set (the GPU box gives a
+    one-GPU job 16 CPUs of a 256-CPU machine; `nproc` reports 16 there)."""
+    n = host_cores()
+    q = _cgroup_cpus()
+    if q:
+        n = min(n, q)
+    omp = _omp_threads()
+    if omp > 0:
+        n = min(n, omp)
     return n
 
 
-def cpu_threads():
-    """Threads of the CPU baseline: the CPU share, at most 16 (the GPU box's
-    share per GPU)."""
-    return max(1, min(cpu_share(), 16))
+def job_cpu_share(world):
+    """CPUs of the whole job at `world` ranks on this node: the affinity set
+    capped by the cgroup quota (shared by the ranks), and by
+    OMP_NUM_THREADS x world where the environment gives each rank a share.
+    torch.distributed.run sets OMP_NUM_THREADS=1 for ranks whose environment
+    does not name one; that default is not a share and is ignored."""
+    if world <= 1:
+        return cpu_share()
+    n = host_cores()
+    q = _cgroup_cpus()
+    if q:
+        n = min(n, q)
+    omp = _omp_threads()
+    if omp > 1:
+        n = min(n, omp * world)
+    return max(1, n)
 
 
-def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
+def cpu_threads(world=1):
+    """Threads of the CPU baseline: the job's CPU share (one GPU: the
+    process's share, 16 on the GPU box; N GPUs: the node share of all N
+    ranks, since the baseline is the node's CPU path beside N GPUs)."""
+    return max(1, job_cpu_share(world))
+
+
+def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample, world=1):
     """Time the CPU codecs of oracle/ on this host, on a bounded sample of
     the same workload, and cross-check them against the GPU parity of the
     same blocks.  `value` is the vectorised encode (oracle/rs_simd.c:
     GFNI+AVX-512 affine or AVX2 split-nibble, ISA-L's published x86
-    techniques), the strongest CPU codec here, on the process's CPU share
-    (cgroup quota / OMP_NUM_THREADS, at most 16: the GPU box's share per
-    GPU), one core beside it, and the scalar table oracle too.  Test
+    techniques), the strongest CPU codec here, on the job's CPU share
+    (job_cpu_share: the process's share at N = 1, the node share of all N
+    ranks at N > 1; the sample grows with the threads so each has blocks),
+    one core beside it, and the scalar table oracle too.  Test
     infrastructure, never the product."""
     from oracle import oracle as O
     O.build()
-    threads = cpu_threads()
-    nb = 128
+    threads = cpu_threads(world)
+    nb = max(128, 2 * threads)
     data = O.aligned_empty((nb, k * S))
     data[:] = O.fill_blocks(SEED, 0, nb, B, k, S)
     par = O.aligned_empty((nb, m * S))
@@ -371,7 +573,8 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                           nb * B, seconds)
     one, _, _ = _rate(lambda: O.encode_simd(k, m, S, data[:64], threads=1, isa=isa, out=par[:64]),
                       64 * B, 1.5)
-    sc_all, _, _ = _rate(lambda: O.encode(k, m, S, data[:32], threads=threads), 32 * B, 2.0)
+    nsc = min(nb, max(32, threads))
+    sc_all, _, _ = _rate(lambda: O.encode(k, m, S, data[:nsc], threads=threads), nsc * B, 2.0)
     sc_one, _, _ = _rate(lambda: O.encode(k, m, S, data[:2], threads=1), 2 * B, 1.0)
     # the rebuild configs (C3): the same blocks, 4 random erasures each,
     # per-block decode rows + the vectorised MAC (oracle/rs_simd.c)
@@ -388,22 +591,25 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample):
                                               isa=isa, out=rout[:16]), 16 * B, 1.0)
     return {"value": round(v, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "sample": "RS(%d,%d) encode, %d x %d-byte blocks x %d passes (%.1f s), vectorised C port "
-                      "(%s, streaming stores) on %d threads (the process's CPU share; %d CPUs in "
-                      "its affinity set); 1-core %.3f GiB/s; scalar table oracle %.3f GiB/s on %d "
-                      "threads, %.3f on 1; bit-exact vs GPU on %d blocks: %s"
-                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, host_cores(), one, sc_all,
-                         threads, sc_one, nchk, ok_simd and ok_scalar),
-            "isa": O.SIMD_ISA[isa], "single_core": round(one, 3),
+                      "(%s, streaming stores) on %d threads (the job's CPU share at %d GPU%s; %d "
+                      "CPUs in the affinity set); 1-core %.3f GiB/s; scalar table oracle %.3f GiB/s "
+                      "on %d threads, %.3f on 1; bit-exact vs GPU on %d blocks: %s"
+                      % (k, m, nb, B, passes, el, O.SIMD_ISA[isa], threads, world,
+                         "" if world == 1 else "s", host_cores(), one, sc_all, threads, sc_one, nchk,
+                         ok_simd and ok_scalar),
+            "isa": O.SIMD_ISA[isa], "single_core": round(one, 3), "n_gpus": world,
+            "per_gpu_share": round(threads / world, 2),
             "cpu_share": cpu_share(), "affinity_cpus": host_cores(),
             "rebuild": {"value": round(rv, 3), "single_core": round(rone, 3), "threads": threads,
                         "erasures": e, "bit_exact": ok_reb,
                         "sample": "RS(%d,%d) rebuild of the same %d blocks, %d random erasures each "
-                                  "(decode rows by Gauss-Jordan + vectorised MAC)" % (k, m, nb, e)},
+                                  "(decode rows by Gauss-Jordan, memoised per pattern, + vectorised MAC)"
+                                  % (k, m, nb, e)},
             "scalar_oracle": {"value": round(sc_all, 3), "single_core": round(sc_one, 3)},
             "bit_exact_vs_gpu": ok_simd and ok_scalar}
 
 
-def c1_case(torch, ec, codec, stream):
+def c1_case(torch, ec, codec, stream, world=1):
     """BASELINE.json configs[0] (C1): RS(3,2) encode + rebuild (e = 1 and 2
     random erasures per block) of 1000 x 64 KiB blocks.  The CPU oracle
     (scalar, 16 host threads; the reference-runnable case) is timed beside
@@ -412,7 +618,7 @@ def c1_case(torch, ec, codec, stream):
     from oracle import oracle as O
     k, m, B, n = 3, 2, 65536, 1000
     S = ec.shard_size(B, k)
-    threads = cpu_threads()
+    threads = cpu_threads(world)
     data = O.fill_blocks(SEED, 0, n, B, k, S)
     t0 = time.perf_counter()
     par = O.encode(k, m, S, data, threads=threads)
@@ -553,7 +759,8 @@ def pmc_traffic(args, result, local, world):
         var, dev = _visible_device(local)
         env[var] = dev
     child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "3", "--warmup", "1",
-             "--settle-ms", "0", "--no-small", "--no-cpu", "--no-e2e", "--no-pmc",
+             "--settle-ms", "0", "--no-small", "--no-cpu", "--no-e2e", "--no-pmc", "--no-verify",
+             "--no-c5",
              "--k", str(k), "--m", str(m), "--block-bytes", str(B), "--blocks", str(n),
              "--erasures", str(e)]
 
@@ -617,13 +824,36 @@ def pmc_traffic(args, result, local, world):
 
 
 def merge_extras(result, extras):
-    """Fold the ranks' side measurements (device copy rate, PCIe end-to-end
-    rates; one dict per rank, rank order) into the contract line (pure:
-    tested on CPU)."""
+    """Fold the ranks' side measurements (one dict per rank, rank order) into
+    the contract line (pure: tested on CPU): the achievable rate of the
+    encode's traffic on each rank's GPU (memo_ec_stream_probe), the
+    whole-batch oracle comparisons of every rank, and the PCIe end-to-end
+    rates."""
     world = len(extras)
     x0 = extras[0]
-    result["roofline"]["copy_GBs"] = round(x0["copy_GBs"], 1)
-    result["roofline"]["frac_of_copy"] = round(result["roofline"]["achieved"] / x0["copy_GBs"], 4)
+    roof = result["roofline"]
+    if "probe" in x0:
+        pr = x0["probe"]
+        roof["achievable"] = pr
+        roof["frac_of_achievable"] = round(roof["achieved"] / pr["GBs"], 4)
+        if "roofline_rebuild" in result:
+            rr = result["roofline_rebuild"]
+            rr["achievable_GBs"] = pr["GBs"]
+            rr["frac_of_achievable"] = round(rr["achieved"] / pr["GBs"], 4)
+        if world > 1:
+            roof["achievable_per_rank_GBs"] = [x["probe"]["GBs"] for x in extras]
+    if "oracle" in x0:
+        par = {}
+        for key in x0["oracle"]:
+            checks = [x["oracle"][key] for x in extras]
+            par[key] = dict(checks[0])
+            par[key]["bit_exact"] = all(c["bit_exact"] for c in checks)
+            par[key]["blocks"] = sum(c["blocks"] for c in checks)
+            par[key]["bytes_compared"] = sum(c["bytes_compared"] for c in checks)
+            par[key]["seconds"] = max(c["seconds"] for c in checks)
+            if world > 1:
+                par[key]["ranks"] = len(checks)
+        result["oracle_parity"] = par
     if "e2e" not in x0:
         return result
     result["end_to_end"] = dict(x0["e2e"])
@@ -639,9 +869,29 @@ def merge_extras(result, extras):
     return result
 
 
+def check_devices(rows, same_device):
+    """Every rank ran on its own GPU: the ranks' PCI bus ids and UUIDs
+    (memo_ec_device_identity) are pairwise distinct, unless the run asked
+    for one shared device (--same-device rehearsals).  Raises otherwise: a
+    node figure from ranks sharing a GPU is not a scaling result."""
+    ids = [r.get("device_identity") for r in rows]
+    if same_device or len(rows) < 2:
+        return
+    if any(i is None for i in ids):
+        raise RuntimeError("bench: a rank reported no device identity")
+    for key in ("pci_bus_id", "uuid"):
+        seen = {}
+        for r, i in zip(rows, ids):
+            if i[key] in seen:
+                raise RuntimeError("bench: ranks %d and %d ran on the same GPU (%s %s)"
+                                   % (seen[i[key]], r["rank"], key, i[key]))
+            seen[i[key]] = r["rank"]
+
+
 def assemble(args, world, rows, wall_max, S):
     """The contract line from the ranks' rows (pure: tested on CPU)."""
     from memo_amd.partition import node_report
+    check_devices(rows, args.same_device)
     k, m, B, n, e, K = args.k, args.m, args.block_bytes, args.blocks, args.erasures, args.steps
     r0 = rows[0]
     step_payload = n * B * (2 if e > 0 else 1)
@@ -687,6 +937,7 @@ def assemble(args, world, rows, wall_max, S):
             "seconds": r["device_seconds"]} for r in rows]
     rep = node_report(per)
     res["ranks"] = {"per_gpu": [{"rank": r["rank"], "device": r["device"],
+                                 **r.get("device_identity", {}),
                                  "GiBs": rep["per_gpu_GiBs"][i],
                                  "encode_kernel_ms": r["encode"]["kernel_ms_avg"],
                                  "encode_frac": r["encode"]["frac"],
@@ -694,9 +945,13 @@ def assemble(args, world, rows, wall_max, S):
                                      "rebuild_frac": r["rebuild"]["frac"]} if e > 0 else {})}
                                 for i, r in enumerate(rows)],
                     "node_sum_GiBs": rep["node_sum_GiBs"],
+                    "distinct_devices": len({(r.get("device_identity") or {}).get("uuid", r["device"])
+                                             for r in rows}),
                     "note": "per-GPU GiB/s = that rank's payload / its own kernel time (HIP events); "
                             "node sum = all payload / the slowest rank's kernel time; `value` = all "
-                            "payload / the job's wall time between barriers"}
+                            "payload / the job's wall time between barriers; pci_bus_id / uuid: "
+                            "memo_ec_device_identity of the rank's GPU (distinct ranks on distinct "
+                            "GPUs unless --same-device)"}
     return res
 
 
@@ -706,8 +961,10 @@ def main():
         # Start the N ranks here, before anything touches a GPU (children,
         # never an exec), one per device; each rank re-enters main().
         from memo_amd.partition import launch_local_ranks
+        # A rank that hangs is killed (by PID) after --rank-timeout seconds
+        # and the launch exits non-zero; the others stop with it.
         sys.exit(launch_local_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus,
-                                    same_device=args.same_device))
+                                    same_device=args.same_device, timeout=args.rank_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
@@ -725,7 +982,10 @@ def main():
         saved = os.dup(1)
         os.dup2(2, 1)
         try:
-            dist_mod.init_process_group("gloo")
+            import datetime
+            # a rank that never reaches a collective fails the others after
+            # --rank-timeout seconds instead of gloo's 30-minute default
+            dist_mod.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.rank_timeout))
         finally:
             sys.stdout.flush()
             os.dup2(saved, 1)
@@ -769,15 +1029,16 @@ def main():
     log("rank %d: inputs resident, timing %d steps" % (rank, args.steps))
     wall, kms, done = timed_steps(torch, fns, args.steps, args.warmup, args.settle_ms, dist, stream)
     codec.synchronize()
-    row = {"rank": rank, "device": local, "warmup_steps_run": done,
+    row = {"rank": rank, "device": local, "device_identity": ec.device_identity(local),
+           "warmup_steps_run": done,
            "payload_bytes": n * B * len(fns) * args.steps,
            "device_seconds": sum(sum(x) for x in kms) * 1e-3,
            "encode": kstats(kms[0], (k + m) * S * n)}
     if e > 0:
         row["rebuild"] = kstats(kms[1], (k + e) * S * n)
         row["rebuild_bit_exact"] = bool(torch.equal(out, want))
-        row["rebuild_kernel"] = ec.rebuild_kernel_name(n, k, S)
-        del surv, out, want
+        row["rebuild_kernel"] = codec.rebuild_kernel_name(n, k, S)
+        del want
     rows = [row]
     wall_max = wall
     if dist is not None:
@@ -795,18 +1056,33 @@ def main():
     result["build_id"] = ec.build_id()
     result["build_matches_sources"] = result["build_id"] == ec.source_id()
 
-    # ---- after the timed steps and their closing barrier: the baselines
-    # and side measurements, at every N.  Every rank measures its own GPU
-    # (device copy, PCIe end-to-end rate over its own link) concurrently;
-    # rank 0 alone times the CPU baseline and the counter passes while the
-    # others wait at the final barrier.
+    # ---- after the timed steps and their closing barrier: the baselines,
+    # checks and side measurements, at every N.  Every rank measures its own
+    # GPU (the achievable rate of the encode's traffic, PCIe end-to-end rate
+    # over its own link) and compares its own whole batch with the CPU
+    # oracle, concurrently; rank 0 alone times the CPU baseline and the
+    # counter passes while the others wait at the final barrier.
     extra = {}
-    # Measured HBM reference on this box: a device-to-device
-    # copy of the same data bytes on the same stream (read + write).
-    scratch = torch.empty_like(data)
-    _, (cms,), _ = timed_steps(torch, [lambda: scratch.copy_(data)], 10, 30, 0, None, stream)
-    extra["copy_GBs"] = 2 * data.numel() / (float(np.median(cms)) * 1e-3) / 1e9
+    # What the memory system allows for this exact traffic (SURVEY.md 8(d)'s
+    # "measured" reference): the encode's tiles and loads/stores, no GF math.
+    scratch = torch.empty_like(par)
+    extra["probe"] = probe_rate(torch, codec, stream, k, m, data, scratch)
     del scratch
+    vthreads = max(1, cpu_threads(world) // world)
+    if not args.no_verify:
+        # Whole-batch parity with the CPU oracle (oracle/rs_simd.c): every
+        # parity byte of the timed encode (C2) and every shard the timed
+        # rebuild produced (C3, this batch's path), on this rank's blocks.
+        log("rank %d: whole-batch oracle comparison" % rank)
+        stage = HostStage(torch)
+        extra["oracle"] = {"C2_encode": verify_encode(stage, k, m, S, data, par, vthreads)}
+        if e > 0:
+            vr = verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, vthreads)
+            vr["path"] = codec.rebuild_path(n, k, S)
+            extra["oracle"]["C3_rebuild"] = vr
+        del stage
+    if e > 0:
+        del surv, out
     if not args.no_e2e:
         if dist is not None:
             dist.barrier()  # all links busy at once, as on a node serving every GPU
@@ -818,14 +1094,31 @@ def main():
         dist.all_gather_object(extras, extra)
     merge_extras(result, extras)
     log("rank %d: timed steps done, side measurements" % rank)
-    if world == 1 and not args.no_small:
-        result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps,
-                                                args.warmup, args.settle_ms)
+    checks = [v["bit_exact"] for v in result.get("oracle_parity", {}).values()]
+    if world == 1:
+        stage = None if args.no_verify else HostStage(torch)
+        if not args.no_small:
+            result["rebuild_small"] = rebuild_small(torch, ec, codec, stream, args.steps, args.warmup,
+                                                    args.settle_ms, stage, vthreads)
+            for v in result["rebuild_small"].values():
+                checks += [v["bit_exact"], v["uniform_pattern"]["bit_exact"]]
+                if "oracle" in v:
+                    checks.append(v["oracle"]["bit_exact"])
+        if not args.no_c5:
+            result["c5_mixed"] = c5_mixed(torch, ec, codec, stream, args.c5_gib, args.steps,
+                                          args.warmup, args.settle_ms, stage, vthreads)
+            checks.append(result["c5_mixed"]["round_trip_bit_exact"])
+            if "oracle_bit_exact" in result["c5_mixed"]:
+                checks.append(result["c5_mixed"]["oracle_bit_exact"])
+        del stage
+    if not args.no_verify:
+        result["oracle_bit_exact"] = bool(checks) and all(checks)
     if rank == 0:
         if not args.no_cpu:
             log("cpu baseline")
-            result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, par[:4].cpu().numpy())
-            result["c1"] = c1_case(torch, ec, codec, stream)
+            result["cpu_baseline"] = cpu_baseline(k, m, B, S, args.cpu_seconds, par[:4].cpu().numpy(),
+                                                  world)
+            result["c1"] = c1_case(torch, ec, codec, stream, world)
         if not args.no_pmc:
             log("counter passes")
             pmc_traffic(args, result, local, world)

@@ -281,8 +281,19 @@ PinnedArena::Lease PinnedArena::lease(size_t bytes) {
   return Lease(this, static_cast<uint8_t*>(p), cap, false);
 }
 
+size_t PinnedArena::kept_bytes() const {
+  std::lock_guard<std::mutex> g(mu_);
+  size_t n = 0;
+  for (auto& b : free_) n += b.cap;
+  return n;
+}
+
 void PinnedArena::put(uint8_t* p, size_t cap, bool pinned) {
   Buf drop{nullptr, 0, false};
+  if (cap > kKeepMaxBytes) {  // an outsized lease is not worth holding pinned
+    release({p, cap, pinned});
+    return;
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     free_.push_back({p, cap, pinned});
@@ -1192,54 +1203,69 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       for (size_t bi = 0; bi < fb.nb; ++bi) fb.S = std::max(fb.S, (size_t)g[grp.ids[b0 + bi]].h.shard_size);
       batches.push_back(std::move(fb));
     }
-  // one survivor and one output lease for the whole call, carved per batch:
-  // a lease per batch held at once took a pinned allocation each beyond the
-  // arena's few kept buffers (~2 ms apiece: 240 ms for 16,384 4 KiB blocks)
-  std::vector<size_t> o_surv(batches.size()), o_out(batches.size());
-  size_t surv_bytes = 0, out_bytes = 0;
-  for (size_t x = 0; x < batches.size(); ++x) {
-    o_surv[x] = surv_bytes;
-    o_out[x] = out_bytes;
-    surv_bytes += (batches[x].nb * k * batches[x].S + 63) & ~(size_t)63;
-    out_bytes += (batches[x].nb * batches[x].grp->e * batches[x].S + 63) & ~(size_t)63;
-  }
-  PinnedArena::Lease surv_all, out_all;
-  if (!batches.empty()) {
-    surv_all = arena_.lease(surv_bytes);
-    out_all = arena_.lease(out_bytes);
-  }
-  const bool pin = batches.empty() || (surv_all.pinned() && out_all.pinned());
-  for (size_t x = 0; x < batches.size(); ++x) {
-    FBatch& fb = batches[x];
-    const int e = fb.grp->e;
-    fb.surv = surv_all.data() + o_surv[x];
-    fb.out = out_all.data() + o_out[x];
-    if (!fb.grp->uniform) {
-      fb.sidx.resize(fb.nb * k);
-      fb.lidx.resize(fb.nb * e);
+  // Chunks of batches with up to stage_bytes of survivors each: one
+  // survivor and one output lease per chunk, carved per batch (a lease per
+  // batch took a pinned allocation each beyond the arena's few kept buffers,
+  // ~2 ms apiece: 240 ms for 16,384 4 KiB blocks), and ONE codec call per
+  // chunk for all its batches (memo_ec_rebuild_segments: a segment per
+  // batch).  A node-loss fetch of thousands of degraded blocks so stages at
+  // most a chunk at a time instead of pinning GBs at once.
+  std::vector<size_t> cuts{0};
+  {
+    size_t acc = 0;
+    for (size_t x = 0; x < batches.size(); ++x) {
+      const size_t sb = batches[x].nb * k * batches[x].S;
+      if (acc > 0 && acc + sb > o_.stage_bytes) {
+        cuts.push_back(x);
+        acc = 0;
+      }
+      acc += sb;
     }
+    if (cuts.back() != batches.size()) cuts.push_back(batches.size());
   }
-  tm.lap("alloc");
-  // (batch, block) pairs copied in on the pool
-  std::vector<std::pair<size_t, size_t>> work;
-  for (size_t x = 0; x < batches.size(); ++x)
-    for (size_t bi = 0; bi < batches[x].nb; ++bi) work.emplace_back(x, bi);
-  pool_.parallel_for(work.size(), [&](size_t t) {
-    FBatch& fb = batches[work[t].first];
-    const size_t bi = work[t].second;
-    Gathered& x = g[fb.grp->ids[fb.b0 + bi]];
-    for (int s = 0; s < k; ++s) {
-      uint8_t* slot = fb.surv + (bi * k + s) * fb.S;
-      std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
-      std::memset(slot + x.h.shard_size, 0, fb.S - x.h.shard_size);
-      if (!fb.grp->uniform) fb.sidx[bi * k + s] = (uint8_t)x.shards[s].first;
+  for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+    const size_t x0 = cuts[ci], x1 = cuts[ci + 1];
+    std::vector<size_t> o_surv(x1 - x0), o_out(x1 - x0);
+    size_t surv_bytes = 0, out_bytes = 0;
+    for (size_t x = x0; x < x1; ++x) {
+      o_surv[x - x0] = surv_bytes;
+      o_out[x - x0] = out_bytes;
+      surv_bytes += (batches[x].nb * k * batches[x].S + 63) & ~(size_t)63;
+      out_bytes += (batches[x].nb * batches[x].grp->e * batches[x].S + 63) & ~(size_t)63;
     }
-    if (!fb.grp->uniform) std::copy(x.lost.begin(), x.lost.end(), fb.lidx.begin() + bi * fb.grp->e);
-  });
-  tm.lap("copy_in");
-  if (!batches.empty()) {
+    PinnedArena::Lease surv_all = arena_.lease(surv_bytes), out_all = arena_.lease(out_bytes);
+    const bool pin = surv_all.pinned() && out_all.pinned();
+    for (size_t x = x0; x < x1; ++x) {
+      FBatch& fb = batches[x];
+      const int e = fb.grp->e;
+      fb.surv = surv_all.data() + o_surv[x - x0];
+      fb.out = out_all.data() + o_out[x - x0];
+      if (!fb.grp->uniform) {
+        fb.sidx.resize(fb.nb * k);
+        fb.lidx.resize(fb.nb * e);
+      }
+    }
+    tm.lap("alloc");
+    // (batch, block) pairs copied in on the pool
+    std::vector<std::pair<size_t, size_t>> work;
+    for (size_t x = x0; x < x1; ++x)
+      for (size_t bi = 0; bi < batches[x].nb; ++bi) work.emplace_back(x, bi);
+    pool_.parallel_for(work.size(), [&](size_t t) {
+      FBatch& fb = batches[work[t].first];
+      const size_t bi = work[t].second;
+      Gathered& x = g[fb.grp->ids[fb.b0 + bi]];
+      for (int s = 0; s < k; ++s) {
+        uint8_t* slot = fb.surv + (bi * k + s) * fb.S;
+        std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
+        std::memset(slot + x.h.shard_size, 0, fb.S - x.h.shard_size);
+        if (!fb.grp->uniform) fb.sidx[bi * k + s] = (uint8_t)x.shards[s].first;
+      }
+      if (!fb.grp->uniform) std::copy(x.lost.begin(), x.lost.end(), fb.lidx.begin() + bi * fb.grp->e);
+    });
+    tm.lap("copy_in");
     std::vector<memo_ec_rebuild_segment> segs;
-    for (auto& fb : batches) {
+    for (size_t x = x0; x < x1; ++x) {
+      const FBatch& fb = batches[x];
       memo_ec_rebuild_segment sg{};
       sg.k = k;
       sg.m = m;
@@ -1255,22 +1281,58 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
     }
     codec_.rebuild_segments(segs, pin);
     tm.lap("rebuild");
+    for (size_t x = x0; x < x1; ++x) decoded_ += batches[x].nb;
+    pool_.parallel_for(work.size(), [&](size_t t) {
+      FBatch& fb = batches[work[t].first];
+      const size_t bi = work[t].second;
+      finish(fb.grp->ids[fb.b0 + bi], fb.out + bi * fb.grp->e * fb.S, fb.S);
+    });
+    tm.lap("assemble");
   }
-  for (auto& fb : batches) decoded_ += fb.nb;
-  pool_.parallel_for(work.size(), [&](size_t t) {
-    FBatch& fb = batches[work[t].first];
-    const size_t bi = work[t].second;
-    finish(fb.grp->ids[fb.b0 + bi], fb.out + bi * fb.grp->e * fb.S, fb.S);
-  });
-  tm.lap("assemble");
   for (size_t i = 0; i < n; ++i) res(addresses[i], std::move(blocks[i]), errs[i]);
 }
 
 void ErasureConsensus::_resign() { backend_->resign(); }
 
-void ErasureConsensus::_remove(const Address& a) {
-  if (a.mutable_block()) return backend_->remove(a);
+// Consensus::remove (Consensus.cc:135-164) -> Paxos::_remove ->
+// Consensus::remove_many (Consensus.cc:178-240): every holder removes what
+// it stores after validating the removal against it (Local::remove ->
+// previous->validate_remove, Local.cc:260-278; for a CHB,
+// CHB::_validate_remove, CHB.cc:203-259, here against the owner the shard
+// header carries), in parallel; unreachable holders are skipped;
+// MissingBlock when no holder removed anything.  A CHB's removal never
+// conflicts (its validation has no conflict outcome), so the reference's
+// re-sign-and-retry loop on Conflict has nothing to retry here.
+void ErasureConsensus::_remove(const Address& a, const RemoveSignature& rs) {
+  if (a.mutable_block()) return backend_->remove(a, rs);
+  const int total = o_.k + o_.m;
+  const ShardKeys keys(a);
+  // (node, shard index; -1: every index) pairs to visit: the placement
+  // index's holders, or, for a block this client has no placement of, the
+  // nodes lookup(address, k+m) names, each asked for every shard
+  struct Target {
+    Node* node;
+    int index;
+  };
+  std::vector<Target> targets;
+  bool known = false;
+  Address owner;
   {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    auto it = index_.find(a);
+    if (it != index_.end()) {
+      known = true;
+      owner = it->second.owner;
+      for (int i = 0; i < (int)it->second.holder.size(); ++i)
+        if (it->second.holder[i])
+          if (auto nd = overlay_.node(it->second.holder[i])) targets.push_back({nd.get(), i});
+    }
+  }
+  if (known) {
+    // every holder would refuse an invalid removal: refuse it before
+    // anything is touched (the shards and the placement stay)
+    const std::string why = chb_validate_remove(a, owner, rs, owners_);
+    if (!why.empty()) throw ValidationFailed("remove " + a.hex() + ": " + why);
     // forget the block first: a repair running concurrently will not
     // re-place it (evict_removed_blocks, tests/doughnut.cc:1693-1719)
     std::vector<Address> old;
@@ -1279,15 +1341,93 @@ void ErasureConsensus::_remove(const Address& a) {
       old = erase_placement_locked(a);
     }
     nodes_.update(a, old, {});
+  } else {
+    for (auto& nd : overlay_.lookup(a, total)) targets.push_back({nd.get(), -1});
   }
-  const ShardKeys keys(a);
-  for (auto& nd : overlay_.lookup(a, (int)overlay_.size()))
-    for (int i = 0; i < o_.k + o_.m; ++i) {
+  std::atomic<int> removed{0};
+  std::mutex emu;
+  std::string refused;
+  std::vector<std::pair<Address, Key>> deferred;  // holders down now
+  pool_.parallel_for(targets.size(), [&](size_t t) {
+    Node* nd = targets[t].node;
+    const int i0 = targets[t].index < 0 ? 0 : targets[t].index;
+    const int i1 = targets[t].index < 0 ? total : targets[t].index + 1;
+    for (int i = i0; i < i1; ++i) {
+      const Key key = keys(i);
       try {
-        nd->remove(keys(i));
-      } catch (Error&) {
+        Buffer head;
+        if (!nd->try_fetch_prefix(key, ShardHeader::kSize, head)) continue;  // not here
+        // the holder's own check, against the owner its shard records (a
+        // header that does not parse is no shard of any block: removed)
+        Address shard_owner = owner;
+        try {
+          shard_owner = decode_shard_header(head.data(), head.size()).owner;
+        } catch (ValidationFailed&) {
+        }
+        const std::string why = chb_validate_remove(a, shard_owner, rs, owners_);
+        if (!why.empty()) {
+          std::lock_guard<std::mutex> g(emu);
+          refused = why;
+          continue;
+        }
+        nd->remove(key);
+        ++removed;
+      } catch (Unavailable&) {
+        // the node is down: remove its shard when it returns (or drop the
+        // debt when it is evicted), so the block does not come back with it
+        if (known) {
+          std::lock_guard<std::mutex> g(emu);
+          deferred.emplace_back(nd->id, key);
+        }
+        if (targets[t].index < 0) break;
+      } catch (silo::MissingKey&) {
       }
     }
+  });
+  if (!deferred.empty()) {
+    std::lock_guard<std::mutex> g(rm_mu_);
+    for (auto& d : deferred) pending_rm_[d.first].push_back(d.second);
+  }
+  if (removed.load() == 0) {
+    if (!refused.empty()) throw ValidationFailed("remove " + a.hex() + ": " + refused);
+    if (!known || deferred.empty()) throw MissingBlock("remove: no shard of " + a.hex());
+  }
+}
+
+size_t ErasureConsensus::pending_removes() const {
+  std::lock_guard<std::mutex> g(rm_mu_);
+  size_t n = 0;
+  for (auto& kv : pending_rm_) n += kv.second.size();
+  return n;
+}
+
+// Shards a removal could not reach on `node` (down at the time): erased now
+// that it is back, or forgotten with its silo when it is evicted.
+void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
+  std::vector<Key> keys;
+  {
+    std::lock_guard<std::mutex> g(rm_mu_);
+    auto it = pending_rm_.find(node);
+    if (it == pending_rm_.end()) return;
+    keys.swap(it->second);
+    pending_rm_.erase(it);
+  }
+  if (evicted) return;
+  auto nd = overlay_.node(node);
+  std::vector<Key> still;
+  for (auto& k : keys) {
+    try {
+      if (nd) nd->remove(k);
+    } catch (Unavailable&) {
+      still.push_back(k);  // down again
+    } catch (silo::MissingKey&) {
+    }
+  }
+  if (!still.empty()) {
+    std::lock_guard<std::mutex> g(rm_mu_);
+    auto& v = pending_rm_[node];
+    v.insert(v.end(), still.begin(), still.end());
+  }
 }
 
 // ------------------------------------------------------------- repair
@@ -1305,9 +1445,8 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     bool skip = false;
   };
   // Chunks of blocks whose survivors are held in memory at once: up to
-  // kChunkBytes of shards (by the recorded block sizes), so that small blocks
+  // stage_bytes of shards (by the recorded block sizes), so that small blocks
   // still fill whole GPU batches per (size, e) group.
-  constexpr size_t kChunkBytes = 512u << 20;
   std::vector<size_t> cuts{0};
   {
     std::shared_lock<std::shared_mutex> g(index_mu_);
@@ -1315,7 +1454,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     for (size_t i = 0; i < blocks.size(); ++i) {
       auto it = index_.find(blocks[i]);
       acc += (size_t)k * memo_ec_shard_size(it == index_.end() ? 0 : it->second.B, k);
-      if (acc >= kChunkBytes && i + 1 - cuts.back() >= (size_t)o_.batch_max) {
+      if (acc >= o_.stage_bytes && i + 1 - cuts.back() >= (size_t)o_.batch_max) {
         cuts.push_back(i + 1);
         acc = 0;
       }
@@ -1607,6 +1746,7 @@ ErasureConsensus::RepairReport ErasureConsensus::evict(const Address& node) {
     std::lock_guard<std::mutex> g(mmu_);
     evict_at_.erase(node);
   }
+  settle_removes(node, true);
   const std::vector<Address> blocks = nodes_.blocks(node);
   ++evictions_;
   return repair_blocks(blocks, false);
@@ -1716,6 +1856,7 @@ void ErasureConsensus::membership_loop() {
       if (mstop_) break;
     }
     bool expand_now = false;
+    std::vector<Address> returned;  // nodes back up: removals owed to them
     while (!mq_.empty()) {
       const auto ev = mq_.front();
       mq_.pop_front();
@@ -1728,6 +1869,7 @@ void ErasureConsensus::membership_loop() {
         // while it was away can take their missing shards now
         evict_at_.erase(ev.second);
         expand_now = expand_now || o_.auto_expand;
+        returned.push_back(ev.second);
       } else if (ev.first == kUnderPlaced) {
         if (under_.empty()) under_at_ = clock::now();
         under_.insert(ev.second);
@@ -1753,8 +1895,9 @@ void ErasureConsensus::membership_loop() {
         ++it;
       }
     }
-    if (due.empty() && !expand_now && retry.empty()) continue;
+    if (due.empty() && !expand_now && retry.empty() && returned.empty()) continue;
     l.unlock();
+    for (auto& id : returned) settle_removes(id, false);
     std::vector<Address> again;
     if (!retry.empty()) {
       // Only blocks still short of k+m owners while some reachable node holds

@@ -116,7 +116,12 @@ class PinnedArena {
     size_t cap_ = 0;
     bool pinned_ = false;
   };
+  // Buffers larger than this are released when their lease ends instead of
+  // kept (the codec stages at most kStageBytes of survivors per call).
+  static constexpr size_t kKeepMaxBytes = (size_t)1 << 30;
   explicit PinnedArena(size_t keep = 8) : keep_(keep) {}
+  // free buffers kept and their bytes (tests)
+  size_t kept_bytes() const;
   ~PinnedArena();
   PinnedArena(const PinnedArena&) = delete;
   PinnedArena& operator=(const PinnedArena&) = delete;
@@ -134,10 +139,14 @@ class PinnedArena {
   };
   void put(uint8_t* p, size_t cap, bool pinned);
   static void release(const Buf& b);
-  std::mutex mu_;
+  mutable std::mutex mu_;
   std::vector<Buf> free_;
   size_t keep_;
 };
+
+// Default survivor bytes one fetch or repair stages (pinned) and hands to
+// one codec call at most (ErasureOptions::stage_bytes).
+constexpr size_t kStageBytes = (size_t)512 << 20;
 
 // ---------------------------------------------------------- shard format
 // On-wire / on-silo shard: a 128-byte header + S payload bytes.  The header
@@ -249,6 +258,9 @@ struct ErasureOptions {
   // the rest to the per-block rebuild.
   int uniform_min = 4;
   size_t uniform_min_bytes = 8u << 20;
+  // Survivor bytes a fetch or repair stages (pinned) per codec call at most;
+  // larger requests run as several such chunks.
+  size_t stage_bytes = kStageBytes;
   // A node that disappears is evicted -- its shards rebuilt elsewhere --
   // after this long unless it comes back ("eviction-delay", Paxos.cc:985-1009,
   // default 10 min, Paxos.hxx:35).  < 0: never automatically.
@@ -309,13 +321,22 @@ class ErasureConsensus : public StackedConsensus {
   void store_many(const std::vector<Block>& blocks);
   const Codec& codec() const { return codec_; }
   uint64_t arena_leases() const { return arena_.leases(); }
+  size_t arena_kept_bytes() const { return arena_.kept_bytes(); }
   const ErasureOptions& options() const { return o_; }
+  // The owner blocks removals of owned CHBs are checked against (the
+  // model's fetch(owner) of CHB::_validate_remove); null: none known, so an
+  // owned CHB's removal needs a valid signature by any key.
+  void set_owner_directory(const OwnerDirectory* d) { owners_ = d; }
+  // Shard removals owed to holders that were down at the removal.
+  size_t pending_removes() const;
 
  protected:
   void _store(const Block& b, StoreMode mode) override;
   std::unique_ptr<Block> _fetch(const Address& a) override;
   void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) override;
-  void _remove(const Address& a) override;
+  // Consensus::remove (Consensus.cc:135-240) with CHB removal semantics
+  // (CHB::_validate_remove, CHB.cc:203-259): see erasure_consensus.cc.
+  void _remove(const Address& a, const RemoveSignature& rs) override;
   // Leaving the network: the mutable blocks' backend hands its blocks off
   // (Paxos::_resign, Paxos.cc:2091-2131, which rebalances mutable blocks
   // only); shards stay where they are, and the remaining nodes' eviction
@@ -372,6 +393,7 @@ class ErasureConsensus : public StackedConsensus {
   std::vector<Address> erase_placement_locked(const Address& a);
   // The repair engine: rebuild and re-place the lost shards of `blocks`.
   RepairReport repair_blocks(const std::vector<Address>& blocks, bool include_down);
+  void settle_removes(const Address& node, bool evicted);
   // membership: overlay events -> the membership thread
   void membership_loop();
   void post(int kind, const Address& id);
@@ -409,6 +431,9 @@ class ErasureConsensus : public StackedConsensus {
   int sub_token_ = -1;
   std::thread mthread_;
   std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0}, evictions_{0};
+  const OwnerDirectory* owners_ = nullptr;
+  mutable std::mutex rm_mu_;
+  std::map<Address, std::vector<Key>> pending_rm_;  // node -> shard keys still to erase
 };
 
 }  // namespace memo_host

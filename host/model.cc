@@ -61,6 +61,90 @@ std::array<uint8_t, 32> sha256(const void* a, size_t na, const void* b, size_t n
   return out;
 }
 
+// ------------------------------------------------------------ remove keys
+namespace {
+struct PKey {
+  EVP_PKEY* k = nullptr;
+  ~PKey() { EVP_PKEY_free(k); }
+};
+struct MdSignCtx {
+  EVP_MD_CTX* c = EVP_MD_CTX_new();
+  ~MdSignCtx() { EVP_MD_CTX_free(c); }
+};
+}  // namespace
+
+KeyPair KeyPair::generate() {
+  PKey p;
+  EVP_PKEY_CTX* c = EVP_PKEY_CTX_new_id(EVP_PKEY_ED25519, nullptr);
+  const bool ok = c && EVP_PKEY_keygen_init(c) == 1 && EVP_PKEY_keygen(c, &p.k) == 1;
+  EVP_PKEY_CTX_free(c);
+  if (!ok) throw Error("ed25519 key generation failed");
+  KeyPair kp;
+  size_t n = 32;
+  kp.public_key.resize(32);
+  kp.private_key.resize(32);
+  if (EVP_PKEY_get_raw_public_key(p.k, kp.public_key.data(), &n) != 1 || n != 32) throw Error("ed25519 key");
+  n = 32;
+  if (EVP_PKEY_get_raw_private_key(p.k, kp.private_key.data(), &n) != 1 || n != 32) throw Error("ed25519 key");
+  return kp;
+}
+
+Buffer KeyPair::sign(const uint8_t* msg, size_t n) const {
+  PKey p;
+  p.k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, nullptr, private_key.data(), private_key.size());
+  MdSignCtx c;
+  Buffer sig(64);
+  size_t len = sig.size();
+  if (!p.k || !c.c || EVP_DigestSignInit(c.c, nullptr, nullptr, nullptr, p.k) != 1 ||
+      EVP_DigestSign(c.c, sig.data(), &len, msg, n) != 1)
+    throw Error("ed25519 signing failed");
+  sig.resize(len);
+  return sig;
+}
+
+bool verify_signature(const Buffer& public_key, const Buffer& signature, const uint8_t* msg,
+                      size_t n) {
+  PKey p;
+  p.k = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, nullptr, public_key.data(), public_key.size());
+  MdSignCtx c;
+  return p.k && c.c && EVP_DigestVerifyInit(c.c, nullptr, nullptr, nullptr, p.k) == 1 &&
+         EVP_DigestVerify(c.c, signature.data(), signature.size(), msg, n) == 1;
+}
+
+void OwnerDirectory::set(const Address& owner, OwnerAcl acl) {
+  std::lock_guard<std::mutex> g(mu_);
+  acl_[owner] = std::move(acl);
+}
+
+std::optional<OwnerAcl> OwnerDirectory::find(const Address& owner) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = acl_.find(owner);
+  if (it == acl_.end()) return std::nullopt;
+  return it->second;
+}
+
+RemoveSignature chb_sign_remove(const Address& chb, const KeyPair& keys) {
+  RemoveSignature rs;
+  rs.signature_key = keys.public_key;
+  rs.signature = keys.sign(chb.value.data(), chb.value.size());
+  return rs;
+}
+
+std::string chb_validate_remove(const Address& chb, const Address& owner,
+                                const RemoveSignature& rs, const OwnerDirectory* dir) {
+  if (!owner) return "";
+  if (!rs.signature_key || !rs.signature) return "Missing field in signature";
+  const Buffer& key = *rs.signature_key;
+  if (!verify_signature(key, *rs.signature, chb.value.data(), chb.value.size()))
+    return "Invalid signature";
+  const std::optional<OwnerAcl> acl = dir ? dir->find(owner) : std::nullopt;
+  if (!acl) return "";  // owner block not found: allowed, as CHB.cc:222-227
+  if (acl->world_write || acl->owner_key == key) return "";
+  for (auto& w : acl->writers)
+    if (w == key) return "";
+  return "Key not found";
+}
+
 Address chb_address(const Buffer& data, const Address& owner, const Buffer& salt,
                     const Version& version) {
   // salt || owner (the owner only when set and version >= 0.4), then data
@@ -370,6 +454,11 @@ bool Node::try_fetch(const Key& k, Buffer& out) const {
   return silo->try_get(k, out);
 }
 
+bool Node::try_fetch_prefix(const Key& k, size_t n, Buffer& out) const {
+  if (!up || evicted) throw Unavailable("node down");
+  return silo->try_get_prefix(k, n, out);
+}
+
 bool Node::has(const Key& k) const { return silo->contains(k); }
 
 namespace {
@@ -569,13 +658,17 @@ std::unique_ptr<Block> ReplicationConsensus::_fetch(const Address& a) {
   throw MissingBlock("missing block " + a.hex());
 }
 
-void ReplicationConsensus::_remove(const Address& a) {
+void ReplicationConsensus::_remove(const Address& a, const RemoveSignature&) {
+  int count = 0;
   for (auto& o : overlay_.lookup(a, factor_)) {
     try {
       o->remove(replica_key(a));
-    } catch (Error&) {
+      ++count;
+    } catch (Unavailable&) {
+    } catch (silo::MissingKey&) {
     }
   }
+  if (!count) throw MissingBlock("remove: no replica of the block");
 }
 
 // ----------------------------------------------------------- configuration

@@ -12,6 +12,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <optional>
 #include <shared_mutex>
 #include <unordered_map>
 #include <mutex>
@@ -128,6 +129,59 @@ Block make_mutable(Address address, Buffer data, int version = 1);
 bool chb_valid(const Address& address, const Buffer& salt, const Address& owner,
                const Buffer& data, const Version& version = kModelVersion);
 
+// ------------------------------------------------------------ remove keys
+// The doughnut's signing keys (Doughnut::keys(), an elle::cryptography RSA
+// pair in memo).  This restatement signs with Ed25519 (OpenSSL EVP): the
+// same sign / verify contract over the same bytes, a smaller key.
+struct KeyPair {
+  Buffer public_key;   // 32 bytes, raw
+  Buffer private_key;  // 32 bytes, raw
+  static KeyPair generate();
+  Buffer sign(const uint8_t* msg, size_t n) const;
+};
+bool verify_signature(const Buffer& public_key, const Buffer& signature, const uint8_t* msg,
+                      size_t n);
+
+// blocks::RemoveSignature (src/memo/model/blocks/Block.hh:21-35): the key
+// that signed the removal and its signature of the block address.  The
+// group fields (group_key, group_index) are left out: groups are mutable
+// ACL blocks, outside this path.
+struct RemoveSignature {
+  std::optional<Buffer> signature_key;
+  std::optional<Buffer> signature;
+};
+
+// What CHB::_validate_remove reads from a CHB's owner block, an ACB
+// (CHB.cc:203-259): the owner key, the keys with write access (ACL
+// entries) and the world-write permission.  model.fetch(owner) is restated
+// as a directory the network's clients share.
+struct OwnerAcl {
+  Buffer owner_key;
+  std::vector<Buffer> writers;
+  bool world_write = false;
+};
+class OwnerDirectory {
+ public:
+  void set(const Address& owner, OwnerAcl acl);
+  std::optional<OwnerAcl> find(const Address& owner) const;
+
+ private:
+  mutable std::mutex mu_;
+  std::map<Address, OwnerAcl> acl_;
+};
+
+// CHB::sign_remove (CHB.cc:140-201): `keys` sign the block address.
+RemoveSignature chb_sign_remove(const Address& chb, const KeyPair& keys);
+// CHB::_validate_remove (CHB.cc:203-259) of a CHB at `chb` owned by `owner`:
+// "" when the removal is allowed, else the failure reason.  No owner:
+// allowed.  Owner set: the signature fields must be present ("Missing field
+// in signature") and verify over the address ("Invalid signature"); an
+// owner block the directory does not know is allowed (the reference warns
+// and allows, CHB.cc:222-227); else the key must be the owner's, a writer's,
+// or the block world-writable ("Key not found").
+std::string chb_validate_remove(const Address& chb, const Address& owner,
+                                const RemoveSignature& rs, const OwnerDirectory* dir);
+
 // ------------------------------------------------------------------- silo
 // silo::Silo (src/memo/silo/Silo.hh:33-129): get/set/erase/list with the
 // MissingKey / Collision contract; subclasses implement _get/_set/_erase/_list.
@@ -242,6 +296,8 @@ struct Node {
   // fetch() that reports a missing key by returning false (no exception);
   // throws Unavailable when the node is down.
   bool try_fetch(const Key& k, Buffer& out) const;
+  // try_fetch() of the value's first n bytes (a shard header).
+  bool try_fetch_prefix(const Key& k, size_t n, Buffer& out) const;
   void remove(const Key& k);
   bool has(const Key& k) const;
 };
@@ -331,7 +387,8 @@ class Consensus {
   void fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
     _fetch(addresses, res);
   }
-  void remove(const Address& a) { _remove(a); }
+  // Consensus::remove(Address, RemoveSignature) (Consensus.cc:135-164).
+  void remove(const Address& a, const RemoveSignature& rs = {}) { _remove(a, rs); }
   // Consensus::resign (Consensus.cc:167-176): the local node is leaving.
   void resign() { _resign(); }
   // Consensus::redundancy / stats (Consensus.cc:350-357): JSON text.
@@ -344,7 +401,7 @@ class Consensus {
   // Default: one fetch per address, errors passed to `res`
   // (Consensus::_fetch, Consensus.cc:108-124).
   virtual void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res);
-  virtual void _remove(const Address& a) = 0;
+  virtual void _remove(const Address& a, const RemoveSignature& rs) = 0;
   virtual void _resign() {}  // Consensus::_resign: nothing by default
 };
 
@@ -372,7 +429,10 @@ class ReplicationConsensus : public Consensus {
   void _store(const Block& b, StoreMode mode) override;
   using Consensus::_fetch;
   std::unique_ptr<Block> _fetch(const Address& a) override;
-  void _remove(const Address& a) override;
+  // Consensus::remove_many (Consensus.cc:178-240) over the `factor` replicas:
+  // unreachable replicas are skipped, MissingBlock when none removed it.
+  // (Mutable blocks' own remove validation is outside this path.)
+  void _remove(const Address& a, const RemoveSignature& rs) override;
 
  private:
   Overlay& overlay_;

@@ -313,6 +313,59 @@ TEST(chb_owner_and_version, false) {
   CHECK(old.address.value[31] == h0[31]);
   CHECK(chb_valid(old.address, salt, owner, data, Version{0, 3, 0}));
 }
+// CHB::sign_remove / CHB::_validate_remove (CHB.cc:140-259): who may remove
+// an owned CHB.
+TEST(chb_remove_validation_rules, false) {
+  const KeyPair owner_k = KeyPair::generate(), writer_k = KeyPair::generate(),
+                other_k = KeyPair::generate();
+  const Address owner = Address::random(flags::mutable_block);
+  Block b = make_chb(bytes("owned"), bytes("s"), owner);
+  Block free_b = make_chb(bytes("unowned"));
+  OwnerDirectory dir;
+  dir.set(owner, OwnerAcl{owner_k.public_key, {writer_k.public_key}, false});
+  // no owner: anyone, signed or not
+  CHECK(chb_validate_remove(free_b.address, free_b.owner, {}, &dir).empty());
+  // owned: the fields must be there and the signature must verify
+  CHECK(chb_validate_remove(b.address, owner, {}, &dir) == "Missing field in signature");
+  RemoveSignature rs = chb_sign_remove(b.address, owner_k);
+  CHECK(chb_validate_remove(b.address, owner, rs, &dir).empty());
+  RemoveSignature bad = rs;
+  (*bad.signature)[3] ^= 1;
+  CHECK(chb_validate_remove(b.address, owner, bad, &dir) == "Invalid signature");
+  // a signature of another block's address does not transfer
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(free_b.address, owner_k), &dir) ==
+        "Invalid signature");
+  // the key needs authority over the owner block: its owner or a writer
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, writer_k), &dir).empty());
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), &dir) ==
+        "Key not found");
+  dir.set(owner, OwnerAcl{owner_k.public_key, {}, true});  // world-writable
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), &dir).empty());
+  // an owner block nobody knows: allowed once the signature verifies (the
+  // reference warns and allows, CHB.cc:222-227)
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), nullptr).empty());
+  CHECK(chb_validate_remove(b.address, owner, {}, nullptr) == "Missing field in signature");
+}
+
+// The pinned arena keeps a few batch buffers for reuse, never one larger
+// than kKeepMaxBytes (a node-loss fetch must not leave GBs pinned).
+TEST(pinned_arena_drops_outsized_buffers, false) {
+  PinnedArena a;
+  {
+    auto big = a.lease(PinnedArena::kKeepMaxBytes + 1);
+    CHECK(big.data() != nullptr);
+  }
+  CHECK(a.kept_bytes() == 0);
+  {
+    auto small = a.lease(1000);
+  }
+  CHECK(a.kept_bytes() == (size_t)1 << 20);
+  {
+    auto again = a.lease(4000);  // reuses the kept buffer
+  }
+  CHECK(a.kept_bytes() == (size_t)1 << 20 && a.leases() == 3);
+}
+
 // -------------------------------------------------------------- GPU tests
 // tests/doughnut.cc:320-335 (CHB): insert -> fetch equal -> remove.
 TEST(CHB, true) {
@@ -326,6 +379,114 @@ TEST(CHB, true) {
   net.ec->remove(b.address);
   CHECK(net.shards(b.address, 14) == 0);
   CHECK_THROW(net.ec->fetch(b.address), MissingBlock);
+}
+
+// Removal of an owned CHB through the plugin (Local::remove ->
+// CHB::_validate_remove at every holder, Local.cc:260-278, CHB.cc:203-259;
+// Consensus::remove_many, Consensus.cc:178-240): unsigned or wrongly signed
+// removals are refused with every shard left in place; the owner's signed
+// removal takes every shard; an address nobody stored is MissingBlock.
+TEST(remove_owned_chb_semantics, true) {
+  Net net(16, 10, 4);
+  OwnerDirectory dir;
+  const KeyPair owner_k = KeyPair::generate(), other_k = KeyPair::generate();
+  const Address owner = Address::random(flags::mutable_block);
+  dir.set(owner, OwnerAcl{owner_k.public_key, {}, false});
+  net.ec->set_owner_directory(&dir);
+  Block b = make_chb(random_bytes(70000, 77), bytes("salt"), owner);
+  net.ec->store(b);
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK_THROW(net.ec->remove(b.address), ValidationFailed);
+  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove(b.address, other_k)), ValidationFailed);
+  RemoveSignature forged = chb_sign_remove(b.address, owner_k);
+  forged.signature_key = other_k.public_key;
+  CHECK_THROW(net.ec->remove(b.address, forged), ValidationFailed);
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+  net.ec->remove(b.address, chb_sign_remove(b.address, owner_k));
+  CHECK(net.shards(b.address, 14) == 0);
+  CHECK_THROW(net.ec->fetch(b.address), MissingBlock);
+  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove(b.address, owner_k)), MissingBlock);
+  CHECK_THROW(net.ec->remove(Address::random(flags::immutable_block)), MissingBlock);
+  // unowned blocks need no signature; a fresh client (no placement of the
+  // block: a restart, index from the silos) removes them from the holders
+  // lookup() names
+  Block u = make_chb(random_bytes(5000, 78));
+  net.ec->store(u);
+  net.o.rescan = false;
+  net.restart();
+  net.ec->remove(u.address);
+  CHECK(net.shards(u.address, 14) == 0);
+}
+
+// A removal while one holder is down: the reachable holders remove their
+// shards at once; the down holder's shard is owed -- erased when the node
+// returns, dropped when it is evicted -- and the eviction repairs nothing
+// of the removed block (evict_removed_blocks, tests/doughnut.cc:1693-1719).
+TEST(remove_with_holder_down, true) {
+  Net net(16, 10, 4);
+  Block a = make_chb(random_bytes(40000, 90)), c = make_chb(random_bytes(40000, 91));
+  net.ec->store(a);
+  net.ec->store(c);
+  std::shared_ptr<Node> down, back;
+  for (auto& n : net.nodes)
+    for (int i = 0; i < 14; ++i)
+      if (n->has(shard_key(a.address, i))) {
+        if (!down) down = n;
+        else if (!back && n != down) back = n;
+      }
+  CHECK(down && back);
+  net.overlay.set_up(down->id, false);
+  net.overlay.set_up(back->id, false);
+  net.ec->remove(a.address);
+  CHECK(net.ec->pending_removes() == 2);
+  CHECK_THROW(net.ec->fetch(a.address), MissingBlock);
+  int left = 0;
+  for (auto& n : net.nodes)
+    for (int i = 0; i < 14; ++i) left += n->has(shard_key(a.address, i));
+  CHECK(left == 2);  // one on each down node
+  // one comes back: its shard goes
+  net.overlay.set_up(back->id, true);
+  CHECK(wait_for([&] { return net.ec->pending_removes() == 1; }));
+  for (int i = 0; i < 14; ++i) CHECK(!back->has(shard_key(a.address, i)));
+  // the other is evicted: its debt goes with its silo; only c is repaired
+  const auto rep = net.ec->evict(down->id);
+  CHECK(net.ec->pending_removes() == 0);
+  CHECK(rep.blocks_checked <= 1);
+  CHECK_THROW(net.ec->fetch(a.address), MissingBlock);
+  CHECK(net.ec->fetch(c.address)->data == c.data);
+  CHECK(net.shards(c.address, 14) == 14);
+}
+
+// A large degraded multi-fetch (a node-loss event) stages its survivors in
+// chunks of at most stage_bytes: one lease pair and one codec call per
+// chunk, every block right, and no outsized pinned buffer kept afterwards.
+TEST(multi_fetch_stages_in_chunks, true) {
+  Net net(16, 10, 4);
+  net.o.stage_bytes = 2u << 20;  // 2 MiB chunks: 20 x 256 KiB blocks' survivors ~ 5 MiB
+  net.o.batch_max = 4;
+  net.restart();
+  std::vector<Block> blocks;
+  for (int i = 0; i < 20; ++i) blocks.push_back(make_chb(random_bytes(256 << 10, 3000 + i)));
+  net.ec->store_many(blocks);
+  int down = 0;
+  for (auto& n : net.nodes)
+    if (down < 2 && !n->silo->list().empty()) {
+      n->up = false;
+      ++down;
+    }
+  std::vector<Address> req;
+  for (auto& b : blocks) req.push_back(b.address);
+  const uint64_t seg0 = net.ec->codec().segments_calls(), leases0 = net.ec->arena_leases();
+  int ok = 0;
+  net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
+    for (auto& x : blocks)
+      if (b && x.address == a && b->data == x.data) ++ok;
+  });
+  CHECK(ok == 20);
+  const uint64_t calls = net.ec->codec().segments_calls() - seg0;
+  CHECK(calls >= 2);                                     // more than one chunk
+  CHECK(net.ec->arena_leases() - leases0 == 2 * calls);  // a lease pair per chunk
 }
 
 // tests/doughnut.cc:361-373 (missing_block).

@@ -110,10 +110,13 @@ typedef struct memo_ec_rebuild_segment {
 } memo_ec_rebuild_segment;
 
 /* Per-context tuning (memo_ec_ctx_set_option).  Each starts from the
- * environment variable named beside it, read once by memo_ec_ctx_create. */
+ * environment variable named beside it, read once by memo_ec_ctx_create;
+ * a value the option refuses is ignored with a warning on stderr. */
 enum memo_ec_option {
     MEMO_EC_OPT_REBUILD_PATH = 1,       /* MEMO_EC_REBUILD_FUSED: -1 auto (default),
-                                           0 decode rows + MAC, 1 fused kernel   */
+                                           0 decode rows + MAC, 1 fused kernel
+                                           (the variable: any value > 0 is 1,
+                                           any value < 0 is auto)                */
     MEMO_EC_OPT_FUSED_MAX_BYTES = 2,    /* MEMO_EC_FUSED_MAX_MB: auto takes the fused
                                            kernel up to this many survivor bytes
                                            per call (256 MiB)                    */
@@ -123,7 +126,9 @@ enum memo_ec_option {
     MEMO_EC_OPT_PIPE_BYTES = 4,         /* MEMO_EC_PIPE_MB: host pipeline batch
                                            (64 MiB)                              */
     MEMO_EC_OPT_COPY_THREADS = 5,       /* MEMO_EC_COPY_THREADS: threads per pageable
-                                           bounce copy (0: the shared pool's all) */
+                                           bounce copy (0: the shared pool's all;
+                                           the variable set to 0 means 1, the
+                                           calling thread only)                  */
     MEMO_EC_OPT_MAX_LAUNCH_TILES = 6,   /* MEMO_EC_MAX_LAUNCH_TILES: tiles per MAC
                                            launch (0: the 31-bit grid limit)     */
     MEMO_EC_OPT_XCD_MIN_TILES = 7,      /* MEMO_EC_XCD_MIN_TILES: smallest segment
@@ -141,6 +146,14 @@ enum memo_ec_option {
  * spreads its batches over them, one ctx per device per host thread
  * (block-index partition, no collective). */
 int memo_ec_device_count(void);
+
+/* Identity of GPU `device`: its PCI bus id ("0000:c1:00.0", pci_len >= 13)
+ * and UUID (32 hex digits, uuid_len >= 33), NUL-terminated into the caller's
+ * buffers.  A node process that spreads batches over the GPUs records these
+ * so a run can prove which physical devices did the work (two ranks naming
+ * the same device is a placement error, not a scaling result). */
+int memo_ec_device_identity(int device, char *pci_bus_id, size_t pci_len,
+                            char *uuid, size_t uuid_len);
 
 /* Context on GPU `device` (its own HIP stream, device scratch). */
 int memo_ec_ctx_create(int device, memo_ec_ctx **out);
@@ -176,6 +189,16 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
                           const uint8_t *surv_idx, const uint8_t *surv,
                           const uint8_t *lost_idx, int e, uint8_t *out,
                           int where);
+
+/* Diagnostic: the memory system's rate for an encode's own traffic.  Runs
+ * the tiles, tile order and non-temporal 16-byte loads / stores that
+ * memo_ec_encode_batch(k = kin, m = r) runs, with the GF arithmetic
+ * replaced by XOR: out shard i of block b = XOR of its kin input shards,
+ * every byte XOR i.  Device pointers only (in n x kin x S, out n x r x S);
+ * asynchronous on the ctx stream.  A launch's rate is the "achievable"
+ * denominator of the codec's roofline (bench.py: frac_of_achievable). */
+int memo_ec_stream_probe(memo_ec_ctx *ctx, int kin, int r, size_t S, size_t n,
+                         const uint8_t *in, uint8_t *out);
 
 /* Page-locked host memory for MEMO_EC_HOST_PINNED calls (hipHostMalloc):
  * batch buffers the caller reuses, so its host-memory calls skip the

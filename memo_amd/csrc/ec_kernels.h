@@ -67,7 +67,8 @@ constexpr int DEC_IDX_REGS = 2;
 // What a MAC launch multiplies with: a precomputed table image (encode), a
 // per-block coefficient row from decode_coef_kernel (two-kernel rebuild), or
 // rows the tile derives from the shard indices itself (fused rebuild).
-enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2 };
+// MAC_PROBE: the same traffic without the GF arithmetic (stream_probe_kernel).
+enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2, MAC_PROBE = 3 };
 
 // LDS bytes of the fused rebuild's decode workspace for a tile of ns blocks:
 // GF log/antilog (1 KiB), LW0 (128 B), per block 3 survivor-mask words + a

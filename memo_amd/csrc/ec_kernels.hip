@@ -1008,6 +1008,41 @@ gf_rebuild_kernel(const MacLaunch L) {
   mac_tile<KC, R, NT, MAC_FUSED>(L.seg[sid], tile, s_tab);
 }
 
+// The memory system's rate for the MAC's own traffic: the tiles, tile
+// order, lane -> column map and non-temporal dwordx4 loads / stores of
+// gf_mac_kernel, with the GF arithmetic replaced by one XOR per shard
+// (output i = XOR of the block's kin inputs, each byte ^ i).  What a launch
+// of this kernel achieves is the denominator of roofline.frac_of_achievable
+// in bench.py (memo_ec_stream_probe).
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256) stream_probe_kernel(const MacLaunch L) {
+  uint32_t sid;
+  uint64_t tile;
+  if (!seg_tile(L, sid, tile)) return;
+  const MacSeg& sg = L.seg[sid];
+  const Unit u = locate(sg, tile);
+  uint4 a = make_uint4(0, 0, 0, 0);
+  for (uint32_t j0 = 0; j0 < sg.kin; j0 += KC) {
+    uint4 d[KC];
+#pragma unroll
+    for (int g = 0; g < KC; ++g)
+      d[g] = j0 + g < sg.kin ? ld16<NT>(u.in(sg, j0 + g)) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int g = 0; g < KC; ++g) {
+      a.x ^= d[g].x;
+      a.y ^= d[g].y;
+      a.z ^= d[g].z;
+      a.w ^= d[g].w;
+    }
+  }
+  if (!u.valid) return;
+#pragma unroll
+  for (int i = 0; i < R; ++i) {
+    const uint32_t b = (uint32_t)i * 0x01010101u;
+    if ((uint32_t)i < sg.r) st16<NT>(u.out(sg, i), make_uint4(a.x ^ b, a.y ^ b, a.z ^ b, a.w ^ b));
+  }
+}
+
 // ------------------------------------------------- closed-form decode rows
 // One LANE per block.  Every shard of the code is a scaled evaluation of
 // one polynomial: with f(z) = sum_j D_j / (z ^ j) over the k data indices
@@ -1763,7 +1798,9 @@ hipError_t launch_sha256(const Sha256Args& a, hipStream_t st) {
 template <int KC, int R>
 static hipError_t launch_mac_t(int mode, const MacLaunch& L, uint32_t grid, size_t lds,
                                hipStream_t st) {
-  if (mode == MAC_FUSED)
+  if (mode == MAC_PROBE)
+    hipLaunchKernelGGL((stream_probe_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), 0, st, L);
+  else if (mode == MAC_FUSED)
     hipLaunchKernelGGL((gf_rebuild_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
   else if (mode == MAC_ROWS)
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, true>), dim3(grid), dim3(256), lds, st, L);

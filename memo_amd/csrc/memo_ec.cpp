@@ -176,8 +176,11 @@ bool get_opt(const memo_ec_opts& o, int opt, int64_t* v) {
   }
 }
 
-// Defaults of a new ctx from the environment (once per memo_ec_ctx_create;
-// unparsable or out-of-range values are ignored).
+// Defaults of a new ctx from the environment (once per memo_ec_ctx_create).
+// The variables keep the meanings they had when each call read them:
+// MEMO_EC_REBUILD_FUSED any nonzero value forces the fused path (negative:
+// auto), MEMO_EC_COPY_THREADS=0 copies on the calling thread only.
+// Unparsable or out-of-range values are ignored with a warning on stderr.
 void read_env_options(memo_ec_opts& o) {
   struct Env {
     const char* name;
@@ -200,10 +203,14 @@ void read_env_options(memo_ec_opts& o) {
     const char* p = std::getenv(e.name);
     if (!p || !*p) continue;
     char* end = nullptr;
-    const long long v = std::strtoll(p, &end, 10);
-    if (end == p) continue;
-    if (v > (LLONG_MAX >> e.shift) || v < -(LLONG_MAX >> e.shift)) continue;
-    (void)set_opt(o, e.opt, (int64_t)v * ((int64_t)1 << e.shift));
+    long long v = std::strtoll(p, &end, 10);
+    bool ok = end != p && v <= (LLONG_MAX >> e.shift) && v >= -(LLONG_MAX >> e.shift);
+    if (ok) {
+      if (e.opt == MEMO_EC_OPT_REBUILD_PATH) v = v < 0 ? -1 : v != 0 ? 1 : 0;
+      if (e.opt == MEMO_EC_OPT_COPY_THREADS && v == 0) v = 1;
+      ok = set_opt(o, e.opt, (int64_t)v * ((int64_t)1 << e.shift));
+    }
+    if (!ok) std::fprintf(stderr, "libmemo_ec: ignoring %s=%s (not a valid value)\n", e.name, p);
   }
 }
 
@@ -1060,6 +1067,29 @@ int memo_ec_device_count(void) {
   return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+int memo_ec_device_identity(int device, char* pci_bus_id, size_t pci_len, char* uuid,
+                            size_t uuid_len) {
+  if (!pci_bus_id || pci_len < 13 || !uuid || uuid_len < 33) return MEMO_EC_EINVAL;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+    return MEMO_EC_ENODEV;
+  const int len = (int)std::min<size_t>(pci_len, 64);
+  HIPCHK(hipDeviceGetPCIBusId(pci_bus_id, len, device));
+  pci_bus_id[len - 1] = '\0';
+  hipDevice_t dev;
+  HIPCHK(hipDeviceGet(&dev, device));
+  hipUUID id{};
+  HIPCHK(hipDeviceGetUuid(&id, dev));
+  static const char kHex[] = "0123456789abcdef";
+  for (int i = 0; i < 16; ++i) {
+    const uint8_t b = (uint8_t)id.bytes[i];
+    uuid[2 * i] = kHex[b >> 4];
+    uuid[2 * i + 1] = kHex[b & 15];
+  }
+  uuid[32] = '\0';
+  return MEMO_EC_OK;
+}
+
 const char* memo_ec_strerror(int code) {
   switch (code) {
     case MEMO_EC_OK: return "ok";
@@ -1198,6 +1228,30 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
                   [&](const uint8_t* src, uint8_t* dst, size_t cnt, hipStream_t st) {
                     return encode_device(c, k, m, S, cnt, src, dst, st);
                   });
+}
+
+int memo_ec_stream_probe(memo_ec_ctx* c, int kin, int r, size_t S, size_t n, const uint8_t* in,
+                         uint8_t* out) {
+  if (!c) return MEMO_EC_EINVAL;
+  if (int rc = check_km(kin, r)) return rc;
+  if (r == 0 || n == 0) return MEMO_EC_OK;
+  if (S == 0 || S % 64 != 0 || !in || !out) return MEMO_EC_EINVAL;
+  if (S >= kMaxShard || too_big(n, (size_t)(kin + r) * S)) return MEMO_EC_ERANGE;
+  DeviceGuard g(c->device);
+  // the encode's geometry for (k, m) = (kin, r), launched as the probe
+  const int R = mac_rbound(r), KC = mac_kchunk(kin, R);
+  const size_t step = max_blocks_per_launch(c, S);
+  for (size_t b0 = 0; b0 < n; b0 += step) {
+    const size_t cnt = std::min(step, n - b0);
+    Plan p = plan_segment((uint32_t)kin, (uint32_t)r, S, cnt, in + b0 * (size_t)kin * S,
+                          (uint64_t)kin * S, S, out + b0 * (size_t)r * S, (uint64_t)r * S, S,
+                          nullptr, 0, KC, R);
+    p.mode = MAC_PROBE;
+    p.lds = 0;
+    std::vector<Plan> plans{p};
+    if (int rc = launch_plans(c, plans, c->stream)) return rc;
+  }
+  return MEMO_EC_OK;
 }
 
 void* memo_ec_host_alloc(size_t bytes) {

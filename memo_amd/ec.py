@@ -76,6 +76,7 @@ EXPORTS = [
     "memo_ec_strerror",
     "memo_ec_version", "memo_ec_device_count", "memo_ec_rebuild_segments",
     "memo_ec_ctx_set_option", "memo_ec_ctx_get_option", "memo_ec_build_id",
+    "memo_ec_device_identity", "memo_ec_stream_probe",
 ]
 
 
@@ -120,6 +121,8 @@ def _lib():
         L.memo_ec_ctx_set_option.argtypes = [ctypes.c_void_p, c_int, ctypes.c_int64]
         L.memo_ec_ctx_get_option.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(ctypes.c_int64)]
         L.memo_ec_build_id.restype = ctypes.c_char_p
+        L.memo_ec_device_identity.argtypes = [c_int, ctypes.c_char_p, _sz, ctypes.c_char_p, _sz]
+        L.memo_ec_stream_probe.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p]
         _LIB = L
     return _LIB
 
@@ -153,6 +156,14 @@ def check_build():
     return b
 
 
+def device_identity(device):
+    """{"pci_bus_id", "uuid"} of GPU `device` (memo_ec_device_identity)."""
+    pci = ctypes.create_string_buffer(64)
+    uid = ctypes.create_string_buffer(64)
+    _check(_lib().memo_ec_device_identity(device, pci, 64, uid, 64), "device_identity")
+    return {"pci_bus_id": pci.value.decode(), "uuid": uid.value.decode()}
+
+
 def shard_size(block_bytes, k):
     """S = round_up(ceil(B / k), 64) -- the shard size of a B-byte block."""
     return _lib().memo_ec_shard_size(block_bytes, k)
@@ -174,33 +185,8 @@ def erasures(seed, first_block, n, k, m, e):
     return s, l[:, :e].copy()
 
 
-def rebuild_path(n=None, k=None, S=None):
-    """Which device rebuild the library runs (memo_ec.cpp rebuild_fused):
-    'fused' -- one gf_rebuild_kernel launch whose tiles derive their blocks'
-    decode rows (calls of up to MEMO_EC_FUSED_MAX_MB = 256 MiB of survivors);
-    'rows' -- decode rows through HBM, then gf_mac_kernel (larger calls).
-    MEMO_EC_REBUILD_FUSED=0/1 forces one."""
-    v = os.environ.get("MEMO_EC_REBUILD_FUSED")
-    if v is not None:
-        return "fused" if _atoi(v) != 0 else "rows"
-    if None in (n, k, S):
-        return "auto"
-    max_mb = _atoi(os.environ.get("MEMO_EC_FUSED_MAX_MB", "256"))
-    return "fused" if n * k * S <= (max_mb << 20) else "rows"
-
-
-def _atoi(v):
-    try:
-        return int(v.strip().split()[0])
-    except (ValueError, IndexError):
-        return 0
-
-
-def rebuild_kernel_name(n=None, k=None, S=None):
-    return {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
-            "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM)",
-            "auto": "fused up to 256 MiB per call, else decode rows + gf_mac_kernel"}[
-        rebuild_path(n, k, S)]
+REBUILD_KERNELS = {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
+                   "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM)"}
 
 
 def _is_torch(x):
@@ -293,6 +279,20 @@ class Codec:
                 for k, v in old.items():
                     self.set_option(k, v)
         return cm()
+
+    def rebuild_path(self, n, k, S):
+        """The device rebuild this ctx runs for n blocks of k survivor shards
+        of S bytes (memo_ec.cpp rebuild_fused, from the ctx's options as set
+        by the environment or set_option): 'fused' (one gf_rebuild_kernel
+        launch whose tiles derive their blocks' decode rows) or 'rows'
+        (decode rows through HBM, then gf_mac_kernel)."""
+        path = self.get_option("rebuild_path")
+        if path >= 0:
+            return "fused" if path else "rows"
+        return "fused" if n * k * S <= self.get_option("fused_max_bytes") else "rows"
+
+    def rebuild_kernel_name(self, n, k, S):
+        return REBUILD_KERNELS[self.rebuild_path(n, k, S)]
 
     # -- codec
     def encode(self, k, m, data, parity, S=None, n=None):
@@ -406,6 +406,14 @@ class Codec:
         _check(_lib().memo_ec_sha256_batch(self._ctx, n, pp or None, pl, ps, _ptr(msg)[0], stride,
                                            lp or None, ul, _ptr(digest)[0]), "sha256")
         return digest
+
+    def stream_probe(self, kin, r, inp, out):
+        """memo_ec_stream_probe: the encode's traffic for (k, m) = (kin, r)
+        without the GF arithmetic (device tensors; asynchronous)."""
+        n, S = _infer_nS(inp, kin)
+        _check(_lib().memo_ec_stream_probe(self._ctx, kin, r, S, n, _ptr(inp)[0], _ptr(out)[0]),
+               "stream_probe")
+        return out
 
     def fill_blocks(self, seed, first_block, n, B, k, S, out):
         _check(_lib().memo_ec_fill_blocks(self._ctx, seed, first_block, n, B, k, S, _ptr(out)[0]),

@@ -47,11 +47,13 @@ int memo_oracle_simd_isa(void)
  * parity of (byte 7-i of the qword) AND x. */
 static uint64_t affine_matrix(uint8_t c)
 {
+    uint8_t col[8];
+    for (int k = 0; k < 8; ++k) col[k] = memo_oracle_gf_mul(c, (uint8_t)(1u << k));
     uint64_t q = 0;
     for (int i = 0; i < 8; ++i) {
         uint8_t row = 0;
         for (int k = 0; k < 8; ++k)
-            if ((memo_oracle_gf_mul(c, (uint8_t)(1u << k)) >> i) & 1) row |= (uint8_t)(1u << k);
+            if ((col[k] >> i) & 1) row |= (uint8_t)(1u << k);
         q |= (uint64_t)row << (8 * (7 - i));
     }
     return q;
@@ -202,7 +204,13 @@ int memo_oracle_encode_simd_mt(int k, int m, size_t S, size_t n, const uint8_t *
  * configs): per block, the decode rows C[lost] * inv(C[surv]) of the scalar
  * oracle (Gauss-Jordan), their affine matrices / nibble tables, then the MAC
  * of block_gfni / block_avx2 over the k survivors.  Layout of
- * memo_ec_rebuild_batch.  Returns the ISA used, or -1 (bad pattern). */
+ * memo_ec_rebuild_batch.  Returns the ISA used, or -1 (bad pattern).
+ *
+ * Each thread memoises the rows and tables of the erasure patterns it has
+ * decoded (a direct-mapped cache keyed by the surv_idx || lost_idx bytes):
+ * a batch of a million 4 KiB blocks holds only C(k+m, e) patterns, and
+ * re-deriving 8x8 bit matrices per block would cost 20x the MAC.  The bytes
+ * are the same either way (the cache holds exactly what a miss computes). */
 typedef struct {
     int isa, k, m, e;
     size_t S, b0, b1;
@@ -211,25 +219,42 @@ typedef struct {
     int rc;
 } rebuild_job;
 
+enum { PAT_CACHE = 8192 };
+
 static void *rebuild_thread(void *arg)
 {
     rebuild_job *r = (rebuild_job *)arg;
-    const int k = r->k, e = r->e;
-    uint8_t *rows = (uint8_t *)malloc((size_t)e * k);
-    uint64_t *aff = (uint64_t *)malloc(sizeof(uint64_t) * (size_t)e * k);
-    uint8_t *nib = (uint8_t *)malloc((size_t)e * k * 32);
-    for (size_t b = r->b0; b < r->b1; ++b) {
-        if (memo_oracle_decode_matrix(k, r->m, r->sidx + b * k, r->lidx + b * e, e, rows)) {
-            r->rc = -1;
-            break;
-        }
-        for (int i = 0; i < e * k; ++i) {
-            if (r->isa == ISA_GFNI512) aff[i] = affine_matrix(rows[i]);
-            else if (r->isa == ISA_AVX2)
-                for (int v = 0; v < 16; ++v) {
-                    nib[(size_t)i * 32 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)v);
-                    nib[(size_t)i * 32 + 16 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)(v << 4));
-                }
+    const int k = r->k, e = r->e, ek = e * k, klen = k + e;
+    /* entry: key (k + e bytes) | valid | rows (e*k) | aff (e*k u64) | nib (e*k*32) */
+    const size_t aff_off = ((size_t)klen + 1 + (size_t)ek + 7) & ~(size_t)7;
+    const size_t ent = aff_off + (size_t)ek * 8 + (r->isa == ISA_AVX2 ? (size_t)ek * 32 : 0);
+    const size_t slots = ek <= 256 ? PAT_CACHE : 1;
+    uint8_t *cache = (uint8_t *)calloc(slots, ent);
+    for (size_t b = r->b0; b < r->b1 && cache; ++b) {
+        const uint8_t *sv = r->sidx + b * k, *lv = r->lidx + b * e;
+        uint32_t h = 2166136261u;
+        for (int i = 0; i < k; ++i) h = (h ^ sv[i]) * 16777619u;
+        for (int i = 0; i < e; ++i) h = (h ^ lv[i]) * 16777619u;
+        uint8_t *c = cache + (size_t)(h & (uint32_t)(slots - 1)) * ent;
+        uint8_t *rows = c + klen + 1;
+        uint64_t *aff = (uint64_t *)(c + aff_off);
+        uint8_t *nib = c + aff_off + (size_t)ek * 8;
+        if (!(c[klen] && memcmp(c, sv, (size_t)k) == 0 && memcmp(c + k, lv, (size_t)e) == 0)) {
+            if (memo_oracle_decode_matrix(k, r->m, sv, lv, e, rows)) {
+                r->rc = -1;
+                break;
+            }
+            for (int i = 0; i < ek; ++i) {
+                if (r->isa == ISA_GFNI512) aff[i] = affine_matrix(rows[i]);
+                else if (r->isa == ISA_AVX2)
+                    for (int v = 0; v < 16; ++v) {
+                        nib[(size_t)i * 32 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)v);
+                        nib[(size_t)i * 32 + 16 + v] = memo_oracle_gf_mul(rows[i], (uint8_t)(v << 4));
+                    }
+            }
+            memcpy(c, sv, (size_t)k);
+            memcpy(c + k, lv, (size_t)e);
+            c[klen] = 1;
         }
         const simd_job j = {r->isa, k, e, r->S, 0, 0, NULL, NULL, rows, aff, nib};
         const uint8_t *d = r->surv + b * (size_t)k * r->S;
@@ -238,8 +263,9 @@ static void *rebuild_thread(void *arg)
         else if (r->isa == ISA_AVX2) block_avx2(&j, d, o);
         else scalar_cols(&j, d, o, 0);
     }
+    if (!cache) r->rc = -1;
     if (r->isa == ISA_GFNI512) sfence_all();
-    free(rows); free(aff); free(nib);
+    free(cache);
     return NULL;
 }
 

@@ -1038,3 +1038,79 @@ def test_ctx_options_round_trip(codec):
         assert codec.get_option(name) == old[name]
     L = ec._lib()
     assert L.memo_ec_ctx_set_option(codec._ctx, 99, 0) == -1
+
+
+def test_env_options_keep_their_meanings(monkeypatch, capfd):
+    """The environment defaults keep what each variable meant when every
+    call read it: any nonzero MEMO_EC_REBUILD_FUSED forces the fused path
+    (negative: auto), MEMO_EC_COPY_THREADS=0 copies on the calling thread
+    only; an unusable value is ignored with a warning on stderr."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from memo_amd import ec
+    for val, want in [("2", 1), ("1", 1), ("0", 0), ("-1", -1), ("-7", -1)]:
+        monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", val)
+        with ec.Codec(0) as c:
+            assert c.get_option("rebuild_path") == want, val
+            assert c.rebuild_path(1, 10, 1 << 30) == ("fused" if want == 1 else "rows")
+    monkeypatch.delenv("MEMO_EC_REBUILD_FUSED")
+    monkeypatch.setenv("MEMO_EC_COPY_THREADS", "0")
+    with ec.Codec(0) as c:
+        assert c.get_option("copy_threads") == 1
+    monkeypatch.setenv("MEMO_EC_COPY_THREADS", "lots")
+    capfd.readouterr()
+    with ec.Codec(0) as c:
+        assert c.get_option("copy_threads") == 0
+    assert "ignoring MEMO_EC_COPY_THREADS=lots" in capfd.readouterr().err
+
+
+def test_rebuild_path_label_follows_ctx_options(codec):
+    """Codec.rebuild_path reads the ctx's own options (bench.py labels its
+    rebuild kernel with it), not the environment."""
+    with codec.options(rebuild_path=-1, fused_max_bytes=1 << 20):
+        assert codec.rebuild_path(16, 10, 4096) == "fused"
+        assert codec.rebuild_path(1024, 10, 4096) == "rows"
+    with codec.options(rebuild_path=1):
+        assert codec.rebuild_path(1 << 20, 10, 1 << 20) == "fused"
+        assert "gf_rebuild_kernel" in codec.rebuild_kernel_name(1 << 20, 10, 1 << 20)
+    with codec.options(rebuild_path=0):
+        assert codec.rebuild_path(1, 10, 64) == "rows"
+
+
+@pytest.mark.parametrize("kin,r,B,n", [(10, 4, 1 << 20, 64), (16, 4, 4096, 3000), (4, 2, 5000, 33),
+                                        (7, 3, 70000, 9), (20, 6, 4096, 100)])
+def test_stream_probe_bytes(codec, kin, r, B, n):
+    """memo_ec_stream_probe writes out shard i of block b = XOR of its kin
+    input shards, every byte XOR i (the encode's traffic without the GF
+    arithmetic), for straight-line and chunked shard counts."""
+    import torch
+    from memo_amd import ec
+    S = ec.shard_size(B, kin)
+    rng = np.random.default_rng(kin * 1000 + n)
+    x = rng.integers(0, 256, size=(n, kin * S), dtype=np.uint8)
+    out = torch.full((n, r * S), 0xA5, dtype=torch.uint8, device="cuda")
+    codec.stream_probe(kin, r, dev(x), out)
+    codec.synchronize()
+    acc = np.bitwise_xor.reduce(x.reshape(n, kin, S), axis=1)
+    want = np.stack([acc ^ np.uint8(i) for i in range(r)], axis=1).reshape(n, r * S)
+    assert np.array_equal(host(out), want)
+
+
+def test_device_identity(codec):
+    """memo_ec_device_identity: the PCI bus id torch reports for cuda:0
+    and a 32-digit UUID; a missing device is ENODEV, short buffers EINVAL."""
+    import ctypes
+    import re
+    import torch
+    from memo_amd import ec
+    ident = ec.device_identity(0)
+    assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", ident["pci_bus_id"])
+    assert re.fullmatch(r"[0-9a-f]{32}", ident["uuid"])
+    props = torch.cuda.get_device_properties(0)
+    if hasattr(props, "pci_bus_id"):
+        assert int(ident["pci_bus_id"].split(":")[1], 16) == props.pci_bus_id
+    L = ec._lib()
+    buf = ctypes.create_string_buffer(64)
+    assert L.memo_ec_device_identity(ec._lib().memo_ec_device_count(), buf, 64, buf, 64) == -5
+    assert L.memo_ec_device_identity(0, buf, 8, buf, 64) == -1

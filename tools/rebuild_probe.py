@@ -47,7 +47,7 @@ def main():
         c.encode(k, m, d, p)
         c.rebuild(k, m, sd, surv, ld, out)
         torch.cuda.synchronize()
-    res = {"k": k, "m": m, "B": B, "n": n, "e": e, "S": S, "path": ec.rebuild_path(),
+    res = {"k": k, "m": m, "B": B, "n": n, "e": e, "S": S, "path": c.rebuild_path(n, k, S),
            "decode_chunks": os.environ.get("MEMO_EC_DECODE_CHUNKS", "default"),
            "decode_table": os.environ.get("MEMO_EC_DECODE_TABLE", "default")}
     for name, fn, alg in (("encode", lambda: c.encode(k, m, d, p), (k + m) * S * n),
