@@ -6,52 +6,20 @@
 
 #include "../../include/memo_ec.h"
 
-// Compile-time knobs.  Each is a measured alternative (DESIGN.md section
-// 4.1; tools/build_variants.sh builds them, tools/tune_mac.py compares them);
-// the defaults are the winners.
-#ifndef MEMO_EC_MAC_NT
-#define MEMO_EC_MAC_NT 1
-#endif
-#ifndef MEMO_EC_MAC_W16
-#define MEMO_EC_MAC_W16 1
-#endif
-#ifndef MEMO_EC_MAC_PAIR
-#define MEMO_EC_MAC_PAIR 1
-#endif
-// 1: straight-line bodies for k = 6, 12, 14 (R <= 4) besides 2, 3, 4, 10, 16
-#ifndef MEMO_EC_MAC_EXTRA_KC
-#define MEMO_EC_MAC_EXTRA_KC 1
-#endif
-
-// 1: rebuild tables built 4 coefficients per lane at once (packed doublings)
-#ifndef MEMO_EC_MAC_COEF4
-#define MEMO_EC_MAC_COEF4 1
-#endif
-// 1: rebuild tables in split q / lo LDS regions with one pad slot per set
-// (bank-conflict-free image stores and per-block set reads); 0: the
-// interleaved 8-dword images of the encode tables
-#ifndef MEMO_EC_MAC_COEF_SOA
-#define MEMO_EC_MAC_COEF_SOA 1
-#endif
-
-#ifndef MEMO_EC_MAC_PAIR16
-#define MEMO_EC_MAC_PAIR16 1
-#endif
-// The same for the k = 16 bodies with per-block tables (rebuild MAC and
-// fused rebuild): pairing takes them from 124 to 153 VGPRs (4 -> 3 waves
-// per SIMD)
-#ifndef MEMO_EC_MAC_PAIR16_COEF
-#define MEMO_EC_MAC_PAIR16_COEF 1
-#endif
-
 namespace memo_ec {
 
-// Streamed shard loads / output stores are non-temporal (read/written once).
-constexpr bool MAC_NT = MEMO_EC_MAC_NT != 0;
-// Fold shards pairwise (three 3-input XORs per 2 coefficients).
-constexpr bool MAC_PAIR = MEMO_EC_MAC_PAIR != 0;
-constexpr bool MAC_COEF4 = MEMO_EC_MAC_COEF4 != 0;
-constexpr bool MAC_COEF_SOA = MEMO_EC_MAC_COEF_SOA != 0;
+// Design choices fixed by measurement (DESIGN.md 4.1 and profiles/HISTORY.md
+// 4.1 hold the rejected alternatives and their numbers; their code is gone):
+//  - streamed shard loads and output stores are non-temporal (read/written
+//    once; plain: 5% slower);
+//  - shards fold pairwise, three 3-input XORs per 2 coefficients, also for
+//    k = 16 (unpaired: 1-3 points slower);
+//  - rebuild tables are built 4 coefficients per lane at once (packed
+//    doublings) into split q / lo LDS regions with one pad slot per set
+//    (the interleaved 8-dword images cost 2/3 of the 4 KiB RS(16,4)
+//    rebuild's LDS cycles in bank conflicts);
+//  - straight-line bodies for k = 6, 12, 14 (R <= 4) besides 2, 3, 4, 10, 16.
+constexpr bool MAC_NT = true;
 // Table dwords per lane staged through registers ahead of the shard loads.
 constexpr int MAC_TAB_REGS = 2;
 // Coefficients per lane staged through registers (rebuild tables built in
@@ -95,7 +63,7 @@ struct MacSeg {
   uint32_t coef_dense;    // 1: per-block rows are exactly R x kpad (kin == kpad, R ==
                           //   coef_rows, coef_bstride == R * kin): slot ci of a tile is
                           //   byte ci of its range
-  uint32_t lo_dw;         // COEF with MAC_COEF_SOA: LDS dword offset of the lo region
+  uint32_t lo_dw;         // per-coefficient tables: LDS dword offset of the lo region
   uint64_t n;             // blocks
   uint64_t tiles;         // tiles (= workgroups) of this segment
   uint64_t tiles_per_block;  // aligned mapping only

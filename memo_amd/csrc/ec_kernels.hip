@@ -173,12 +173,11 @@ __device__ __forceinline__ void lookups(const Sel& s, const Tab& t, uint32_t& pl
 template <int KC, int R, bool SOA>
 __device__ __forceinline__ void mac_chunk(uint32_t (&acc)[R][4], const uint4 (&d)[KC],
                                           const TabRef<SOA>& tab, uint32_t kpad, uint32_t j0) {
-  // Pairing costs 12 selector VGPRs: the k = 16 body keeps 4 waves per
-  // SIMD only without it (MEMO_EC_MAC_PAIR16).
-  constexpr bool PAIR = MAC_PAIR && (KC != 16 || (SOA ? MEMO_EC_MAC_PAIR16_COEF : MEMO_EC_MAC_PAIR16));
+  // Pairing costs 12 selector VGPRs (the k = 16 bodies: 3 waves per SIMD
+  // instead of 4) and still wins (profiles/r02_w16_occupancy_ab.jsonl).
 #pragma unroll
-  for (int g = 0; g < KC; g += PAIR ? 2 : 1) {
-    const bool two = PAIR && g + 1 < KC;
+  for (int g = 0; g < KC; g += 2) {
+    const bool two = g + 1 < KC;
     Sel sa[4], sb[4];
     sa[0] = make_sel(d[g].x);
     sa[1] = make_sel(d[g].y);
@@ -334,7 +333,7 @@ __device__ __forceinline__ bool seg_tile(const MacLaunch& L, uint32_t& sid, uint
 }
 
 // ---- Rebuild tables built in LDS from per-block decode coefficients.
-// Layout (MAC_COEF_SOA): the images of a tile's table sets are split into a
+// Layout: the images of a tile's table sets are split into a
 // q region (mid0 mid1 hi0 hi1: 16 B per slot) and a lo region (4 B per
 // slot), each set followed by one pad slot.  Consecutive slots' image stores
 // are then bank-conflict-free (16-B / 4-B strides), and the 2-4 sets one
@@ -395,14 +394,9 @@ __device__ __forceinline__ void coef_image4(uint32_t c4, uint4 (&q)[4], uint32_t
 // Store the image of slot ci (per = R * kpad slots per set).
 __device__ __forceinline__ void put_image(uint32_t* s_tab, const MacSeg& sg, uint32_t per,
                                           uint32_t ci, const uint4& q, uint32_t lo) {
-  if constexpr (MAC_COEF_SOA) {
-    const uint32_t x = ci + ci / per;  // one pad slot per set
-    *reinterpret_cast<uint4*>(s_tab + 4 * x) = q;
-    s_tab[sg.lo_dw + x] = lo;
-  } else {
-    *reinterpret_cast<uint4*>(s_tab + 8 * ci) = q;
-    *reinterpret_cast<uint4*>(s_tab + 8 * ci + 4) = make_uint4(lo, 0, 0, 0);
-  }
+  const uint32_t x = ci + ci / per;  // one pad slot per set
+  *reinterpret_cast<uint4*>(s_tab + 4 * x) = q;
+  s_tab[sg.lo_dw + x] = lo;
 }
 
 // Coefficient of table-image slot ci (set, row i, column j; kpad columns per
@@ -474,35 +468,22 @@ __device__ __forceinline__ void store_images(const MacSeg& sg, const Unit& u,
 #pragma unroll
   for (int q = 0; q < MAC_COEF_REGS; ++q)
     cv[q] = coef_slot_ok<R, KP>(sg, t + 256u * q, total) ? cv0[q] : 0u;
-  if constexpr (MAC_COEF4) {
-    static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
-    if (t < total) {  // waves past the tile's slots skip the build
-      uint4 q[4];
-      uint32_t lo[4];
-      coef_image4(pack4(cv[0], cv[1], cv[2], cv[3]), q, lo);
+  static_assert(MAC_COEF_REGS == 6, "two packed groups: slots t + 256 * (0..3), (4..5)");
+  if (t < total) {  // waves past the tile's slots skip the build
+    uint4 q[4];
+    uint32_t lo[4];
+    coef_image4(pack4(cv[0], cv[1], cv[2], cv[3]), q, lo);
 #pragma unroll
-      for (uint32_t a = 0; a < 4; ++a)
-        if (t + 256u * a < total) put_image(s_tab, sg, R * KP, t + 256u * a, q[a], lo[a]);
-    }
-    if (t + 1024u < total) {
-      uint4 q[4];
-      uint32_t lo[4];
-      coef_image4(pack4(cv[4], cv[5], 0, 0), q, lo);
+    for (uint32_t a = 0; a < 4; ++a)
+      if (t + 256u * a < total) put_image(s_tab, sg, R * KP, t + 256u * a, q[a], lo[a]);
+  }
+  if (t + 1024u < total) {
+    uint4 q[4];
+    uint32_t lo[4];
+    coef_image4(pack4(cv[4], cv[5], 0, 0), q, lo);
 #pragma unroll
-      for (uint32_t a = 0; a < 2; ++a)
-        if (t + 256u * (4 + a) < total) put_image(s_tab, sg, R * KP, t + 256u * (4 + a), q[a], lo[a]);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < MAC_COEF_REGS; ++k) {
-      const uint32_t ci = t + 256u * k;
-      if (ci < total) {
-        uint4 q;
-        uint32_t lo;
-        coef_image(cv[k], q, lo);
-        put_image(s_tab, sg, R * KP, ci, q, lo);
-      }
-    }
+    for (uint32_t a = 0; a < 2; ++a)
+      if (t + 256u * (4 + a) < total) put_image(s_tab, sg, R * KP, t + 256u * (4 + a), q[a], lo[a]);
   }
 }
 
@@ -864,7 +845,7 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   const uint32_t set_dw = R * kpad * 8;
 
   const Unit u = locate(sg, tile);
-  constexpr bool SOA = COEF && MAC_COEF_SOA;
+  constexpr bool SOA = COEF;  // per-coefficient tables: split q / lo regions
   TabRef<SOA> tab;
   if constexpr (SOA) {
     const uint32_t x0 = sg.coef_bstride ? u.set * (R * kpad + 1) : 0u;  // padded slot of set
@@ -979,17 +960,9 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   }
 }
 
-// Minimum waves per SIMD asked of the register allocator: 1 leaves it free;
-// MEMO_EC_MAC_W16 pins the (16, R<=4) instances (132 VGPRs, 3 waves free).
-template <int KC, int R>
-constexpr int mac_min_waves() {
-  return (KC == 16 && R <= 4) ? MEMO_EC_MAC_W16 : 1;
-}
-
 // Encode (MAC_ENCODE) and the two-kernel rebuild's MAC (MAC_ROWS).
 template <int KC, int R, bool NT, bool COEF>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(mac_min_waves<KC, R>())))
-gf_mac_kernel(const MacLaunch L) {
+__global__ void __launch_bounds__(256) gf_mac_kernel(const MacLaunch L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
   uint32_t sid;
   uint64_t tile;
@@ -999,8 +972,7 @@ gf_mac_kernel(const MacLaunch L) {
 
 // Rebuild in one launch: decode rows derived per tile, then the MAC.
 template <int KC, int R, bool NT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(mac_min_waves<KC, R>())))
-gf_rebuild_kernel(const MacLaunch L) {
+__global__ void __launch_bounds__(256) gf_rebuild_kernel(const MacLaunch L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
   uint32_t sid;
   uint64_t tile;
@@ -1833,9 +1805,7 @@ int mac_rbound(int r) {
 int mac_kchunk(int kin, int R) {
   switch (kin) {
     case 2: case 3: case 4: case 10: case 16: return kin;
-#if MEMO_EC_MAC_EXTRA_KC
     case 6: case 12: case 14: return R <= 4 ? kin : 4;  // instantiated for R <= 4 only
-#endif
     default: return 4;
   }
 }
@@ -1861,11 +1831,9 @@ hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid
     case 3: return launch_mac_r<3>(R, mode, L, grid, lds, st);
     case 4: return launch_mac_r<4>(R, mode, L, grid, lds, st);
     case 10: return launch_mac_r<10>(R, mode, L, grid, lds, st);
-#if MEMO_EC_MAC_EXTRA_KC
     case 6: return launch_mac_r4<6>(R, mode, L, grid, lds, st);
     case 12: return launch_mac_r4<12>(R, mode, L, grid, lds, st);
     case 14: return launch_mac_r4<14>(R, mode, L, grid, lds, st);
-#endif
     case 16: return launch_mac_r<16>(R, mode, L, grid, lds, st);
     default: return hipErrorInvalidValue;
   }

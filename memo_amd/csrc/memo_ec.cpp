@@ -265,10 +265,10 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   s.n = n; s.kin = kin; s.r = r;
   s.kpad = kpad_of(kin, KC);
   s.chunks = (uint32_t)(S / 16);
-  // LDS per table set: 8-dword images, or (rebuild, MAC_COEF_SOA) 16-B q +
-  // 4-B lo per slot plus one pad slot (ec_kernels.hip: put_image)
+  // LDS per table set: 8-dword images, or (per-coefficient tables: rebuild)
+  // 16-B q + 4-B lo per slot plus one pad slot (ec_kernels.hip: put_image)
   const size_t per = (size_t)R * s.kpad;
-  const bool soa = per_coef && MAC_COEF_SOA;
+  const bool soa = per_coef;
   const size_t set_bytes = soa ? (per + 1) * 20 : per * 32;
   const uint64_t C = s.chunks;
   uint64_t sets;
