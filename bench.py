@@ -67,6 +67,8 @@ def parse(argv=None):
     ap.add_argument("--blocks", type=int, default=4096, help="blocks per GPU")
     ap.add_argument("--erasures", type=int, default=4)
     ap.add_argument("--no-small", action="store_true", help="skip the 4 KiB random-rebuild lines")
+    ap.add_argument("--small-only", action="store_true",
+                    help=argparse.SUPPRESS)  # the counter pass child of pmc_small: 4 KiB lines only
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-pmc", action="store_true",
@@ -218,7 +220,8 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             "points": points, "fused": fused}
 
 
-def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms, stage=None, threads=1):
+def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms, stage=None, threads=1,
+                  uniform=True):
     """Small-block rebuild: 4 KiB blocks (~4 GiB of payload), 4 random
     erasures per block, so every block has its own decode rows and a
     256-column tile spans up to 17 blocks.  Encode of the same blocks is
@@ -262,6 +265,10 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms, stage=None
                "bit_exact": ok}
         if stage is not None:
             row["oracle"] = verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, threads)
+        res["RS(%d,%d)" % (k, m)] = row
+        if not uniform:
+            del d, p, surv, out, want, sd, ld
+            continue
         # the repair case: one lost node, every block the same pattern
         # (memo_ec_rebuild_uniform), here block 0's
         su, lu = s_idx[0], l_idx[0]
@@ -277,7 +284,6 @@ def rebuild_small(torch, ec, codec, stream, steps, warmup, settle_ms, stage=None
                                   "frac": round(alg / (ums * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
                                   "bit_exact": bool(torch.equal(out, want)),
                                   "check": "every rebuilt shard == the original shard it replaces"}
-        res["RS(%d,%d)" % (k, m)] = row
         log("rebuild_small RS(%d,%d): %.3f of peak, %.3f of achievable" % (
             k, m, row["frac"], row["frac_of_achievable"]))
         del d, p, surv, out, want, sd, ld, sdu, ldu
@@ -823,6 +829,87 @@ def pmc_traffic(args, result, local, world):
         result["roofline_rebuild"]["traffic_source"] = src
 
 
+SMALL_PMC = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_ACTIVE_INST_ANY",
+             "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"]
+
+
+def pmc_small(args, result, local, world):
+    """One rocprofv3 counter pass over a child run of the 4 KiB lines (the
+    per-block-pattern rebuild and the encode of the same blocks, both codes)
+    and, per kernel, what bounds it: valu_busy = SQ_INSTS_VALU x 2 cycles (a
+    wave64 VALU instruction holds a SIMD-32 for 2) over the 1024 SIMDs'
+    cycles (GRBM_GUI_ACTIVE / 8 XCDs = the dispatch's cycles at its own
+    clock, MI355X_MICROARCH.md), and each wave's split into issuing,
+    issue-stalled and parked (waitcnt / barrier) cycles."""
+    import csv
+    import glob
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    rocprof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    env = {x: v for x, v in os.environ.items()
+           if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "MASTER_ADDR", "MASTER_PORT") and not x.startswith("TORCHELASTIC")}
+    if world > 1 and not args.same_device:
+        var, dev = _visible_device(local)
+        env[var] = dev
+    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--small-only", "--steps", "3",
+             "--warmup", "1", "--settle-ms", "0"]
+    tmp = tempfile.mkdtemp(prefix="memo_pmc_small_", dir=os.environ.get("TMPDIR", "/tmp"))
+    vals = {}
+    try:
+        d = os.path.join(tmp, "sq")
+        r = subprocess.run([rocprof, "--pmc"] + SMALL_PMC + ["-d", d, "-o", "pmc", "-f", "csv", "--"] + child,
+                           env=env, cwd=tmp, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=240)
+        files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+        if r.returncode != 0 or not files:
+            raise RuntimeError("rocprofv3: rc %d, %s" % (r.returncode, r.stderr.decode(errors="replace")[-300:]))
+        for f in files:
+            with open(f) as fh:
+                for row in csv.DictReader(fh):
+                    name = row.get("Kernel_Name", "")
+                    mm = re.search(r"gf_mac_kernel<(\d+), (\d+), \w+, (true|false)>", name)
+                    md = re.search(r"decode_\w*kernel<(\d+)", name)
+                    if mm:
+                        key = (int(mm.group(1)), "rebuild MAC" if mm.group(3) == "true" else "encode MAC")
+                    elif md:
+                        key = (int(md.group(1)), "decode rows")
+                    else:
+                        continue
+                    vals.setdefault(key, {}).setdefault((row.get("Dispatch_Id"), ), {})[
+                        row["Counter_Name"]] = float(row["Counter_Value"])
+    except (OSError, RuntimeError, subprocess.SubprocessError, KeyError, ValueError) as ex:
+        result.setdefault("rebuild_small", {})["counters_note"] = "counter pass failed: %s" % str(ex)[:300]
+        return
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+    def summary(disp):
+        def med(c):
+            v = [x[c] for x in disp.values() if c in x]
+            return float(np.median(v)) if v else 0.0
+        waves = med("SQ_WAVES") or 1.0
+        cycles = med("GRBM_GUI_ACTIVE") / 8
+        out = {"valu_busy": round(med("SQ_INSTS_VALU") * 2 / (1024 * cycles), 4) if cycles else None,
+               "valu_per_wave": round(med("SQ_INSTS_VALU") / waves, 1),
+               "salu_per_wave": round(med("SQ_INSTS_SALU") / waves, 1),
+               "lds_per_wave": round(med("SQ_INSTS_LDS") / waves, 1),
+               "issuing_cycles_per_wave": round(4 * med("SQ_ACTIVE_INST_ANY") / waves),
+               "issue_stalled_cycles_per_wave": round(4 * med("SQ_WAIT_INST_ANY") / waves),
+               "parked_cycles_per_wave": round(4 * med("SQ_WAIT_ANY") / waves),
+               "dispatches": len(disp)}
+        return out
+
+    for (kc, kind), disp in sorted(vals.items()):
+        name = {16: "RS(16,4)", 10: "RS(10,4)"}.get(kc)
+        if name and name in result.get("rebuild_small", {}):
+            result["rebuild_small"][name].setdefault("counters", {})[kind] = summary(disp)
+    result.setdefault("rebuild_small", {})["counters_source"] = (
+        "rocprofv3 --pmc %s, one pass over a child run of the same 4 KiB lines (3 steps), per-dispatch "
+        "medians; valu_busy = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)" % " ".join(SMALL_PMC))
+
+
 def merge_extras(result, extras):
     """Fold the ranks' side measurements (one dict per rank, rank order) into
     the contract line (pure: tested on CPU): the achievable rate of the
@@ -1007,6 +1094,10 @@ def main():
     codec = ec.Codec(local)
     codec.set_stream(stream)
     assert codec.stream == stream.cuda_stream and stream.cuda_stream
+    if args.small_only:  # the child of pmc_small: the 4 KiB lines, nothing else
+        rebuild_small(torch, ec, codec, stream, args.steps, args.warmup, args.settle_ms, uniform=False)
+        codec.close()
+        return
 
     data = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
     par = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
@@ -1122,6 +1213,8 @@ def main():
         if not args.no_pmc:
             log("counter passes")
             pmc_traffic(args, result, local, world)
+            if "rebuild_small" in result:
+                pmc_small(args, result, local, world)
         if args.sha:
             result["sha256"] = sha_lines(torch, codec, stream, data, n, B)
         if args.sweep and world == 1:

@@ -156,6 +156,13 @@ def test_bench_assemble_per_rank_fields():
     assert res["oracle_parity"]["C3_rebuild"]["bit_exact"] is True
     assert [p["pci_bus_id"] for p in res["ranks"]["per_gpu"]] == ["0000:11:00.0", "0000:12:00.0"]
     assert res["ranks"]["distinct_devices"] == 2
+    # the same rows naming one GPU twice: no line (unless --same-device)
+    dup = [dict(r) for r in rows]
+    dup[1]["device_identity"] = dict(dup[0]["device_identity"])
+    with pytest.raises(RuntimeError, match="same GPU"):
+        bench.assemble(args, 2, dup, 0.05, S)
+    same = bench.parse(["--gpus", "2", "--same-device", "--blocks", "4096", "--steps", "10"])
+    assert bench.assemble(same, 2, dup, 0.05, S)["ranks"]["distinct_devices"] == 1
     assert res["end_to_end"]["pinned"]["value"] == 48.0
     assert res["end_to_end"]["node_sum"] == {"pinned": 95.0, "pageable": 89.0}
     assert [x["rank"] for x in res["end_to_end"]["per_rank"]] == [0, 1]
