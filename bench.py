@@ -460,16 +460,29 @@ def verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, threads):
 
 
 def probe_rate(torch, codec, stream, kin, r, inp, out, launches=10, warmup=5):
-    """Achievable rate of the MAC's own traffic on this GPU: memo_ec_stream_probe
-    (the same tiles and 16-byte non-temporal loads / stores, XOR in place of
-    the GF arithmetic) over the same buffers, HIP events on `stream`."""
+    """What the memory system allows for the MAC's own traffic on this GPU
+    (memo_ec_stream_probe: the same tiles and 16-byte non-temporal loads /
+    stores, XOR in place of the GF arithmetic, over the same buffers; HIP
+    events on `stream`).  `GBs` / `frac` (the achievable denominator): the
+    read-only and the write-only launches' times added -- this mix of read
+    and write streams without the cost of interleaving them.  `copy`: both
+    in one launch, as a naive streaming kernel interleaves them."""
     n, S = inp.shape[0], inp.shape[1] // kin
-    _, (pms,), _ = timed_steps(torch, [lambda: codec.stream_probe(kin, r, inp, out)], launches,
-                               warmup, 0, None, stream)
-    ms = float(np.mean(pms))
-    return {"kernel": "stream_probe_kernel (the MAC's loads/stores, XOR only)",
-            "GBs": round((kin + r) * S * n / (ms * 1e-3) / 1e9, 1), "kernel_ms_avg": round(ms, 4),
-            "frac": round((kin + r) * S * n / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}
+    alg = (kin + r) * S * n
+    ms = {}
+    for mode in ("read", "write", "copy"):
+        _, (pms,), _ = timed_steps(torch, [lambda: codec.stream_probe(kin, r, inp, out, mode)], launches,
+                                   warmup, 0, None, stream)
+        ms[mode] = float(np.mean(pms))
+    t = ms["read"] + ms["write"]
+    gbs = lambda b, x: round(b / (x * 1e-3) / 1e9, 1)  # noqa: E731
+    return {"kernel": "stream_probe_kernel (the MAC's loads / stores, XOR only): read-only + write-only "
+                      "launches", "GBs": gbs(alg, t), "frac": round(alg / (t * 1e-3) / 1e9 / PEAK_HBM_GBS, 4),
+            "kernel_ms_avg": round(t, 4),
+            "read": {"ms": round(ms["read"], 4), "GBs": gbs(kin * S * n, ms["read"])},
+            "write": {"ms": round(ms["write"], 4), "GBs": gbs(r * S * n, ms["write"])},
+            "copy": {"ms": round(ms["copy"], 4), "GBs": gbs(alg, ms["copy"]),
+                     "frac": round(alg / (ms["copy"] * 1e-3) / 1e9 / PEAK_HBM_GBS, 4)}}
 
 
 def _rate(fn, nbytes, seconds):

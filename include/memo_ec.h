@@ -193,12 +193,21 @@ int memo_ec_rebuild_batch(memo_ec_ctx *ctx, int k, int m, size_t S, size_t n,
 /* Diagnostic: the memory system's rate for an encode's own traffic.  Runs
  * the tiles, tile order and non-temporal 16-byte loads / stores that
  * memo_ec_encode_batch(k = kin, m = r) runs, with the GF arithmetic
- * replaced by XOR: out shard i of block b = XOR of its kin input shards,
- * every byte XOR i.  Device pointers only (in n x kin x S, out n x r x S);
- * asynchronous on the ctx stream.  A launch's rate is the "achievable"
- * denominator of the codec's roofline (bench.py: frac_of_achievable). */
+ * replaced by XOR.  mode MEMO_EC_PROBE_COPY: out shard i of block b = XOR
+ * of its kin input shards, every byte XOR i; MEMO_EC_PROBE_READ: the loads
+ * alone (out unspecified); MEMO_EC_PROBE_WRITE: the stores alone (out
+ * unspecified).  Device pointers only (in n x kin x S, out n x r x S);
+ * asynchronous on the ctx stream.  The read and write launches' times
+ * added give the "achievable" rate of the codec's roofline: this mix of
+ * read and write streams without the cost of interleaving them (bench.py:
+ * roofline.achievable, frac_of_achievable). */
+enum memo_ec_probe_mode {
+    MEMO_EC_PROBE_COPY = 0,
+    MEMO_EC_PROBE_READ = 1,
+    MEMO_EC_PROBE_WRITE = 2
+};
 int memo_ec_stream_probe(memo_ec_ctx *ctx, int kin, int r, size_t S, size_t n,
-                         const uint8_t *in, uint8_t *out);
+                         const uint8_t *in, uint8_t *out, int mode);
 
 /* Page-locked host memory for MEMO_EC_HOST_PINNED calls (hipHostMalloc):
  * batch buffers the caller reuses, so its host-memory calls skip the

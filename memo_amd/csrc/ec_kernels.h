@@ -79,6 +79,7 @@ struct MacSeg {
   uint32_t* status;       // set to 1 on an invalid survivor / lost index set
   uint32_t m;             // parity shards of the code (kin + m = shard count)
   uint32_t ws_dw;         // LDS dword offset of the decode workspace
+  uint32_t probe;         // stream_probe_kernel: a memo_ec_probe_mode
 };
 
 struct MacLaunch {

@@ -983,9 +983,13 @@ __global__ void __launch_bounds__(256) gf_rebuild_kernel(const MacLaunch L) {
 // The memory system's rate for the MAC's own traffic: the tiles, tile
 // order, lane -> column map and non-temporal dwordx4 loads / stores of
 // gf_mac_kernel, with the GF arithmetic replaced by one XOR per shard
-// (output i = XOR of the block's kin inputs, each byte ^ i).  What a launch
-// of this kernel achieves is the denominator of roofline.frac_of_achievable
-// in bench.py (memo_ec_stream_probe).
+// (output i = XOR of the block's kin inputs, each byte ^ i).  sg.probe
+// picks the traffic: MEMO_EC_PROBE_COPY both, MEMO_EC_PROBE_READ the loads
+// alone (the XOR kept live by a store that practically never happens),
+// MEMO_EC_PROBE_WRITE the stores alone (a per-lane pattern).  bench.py's
+// roofline.achievable is the read and write launches' times added: the
+// rate this mix of read and write streams gets when they do not interleave
+// (memo_ec_stream_probe).
 template <int KC, int R, bool NT>
 __global__ void __launch_bounds__(256) stream_probe_kernel(const MacLaunch L) {
   uint32_t sid;
@@ -993,21 +997,28 @@ __global__ void __launch_bounds__(256) stream_probe_kernel(const MacLaunch L) {
   if (!seg_tile(L, sid, tile)) return;
   const MacSeg& sg = L.seg[sid];
   const Unit u = locate(sg, tile);
-  uint4 a = make_uint4(0, 0, 0, 0);
-  for (uint32_t j0 = 0; j0 < sg.kin; j0 += KC) {
-    uint4 d[KC];
+  uint4 a = make_uint4((uint32_t)tile, threadIdx.x, 0x9e3779b9u, 0x7f4a7c15u);
+  if (sg.probe != MEMO_EC_PROBE_WRITE) {
+    a = make_uint4(0, 0, 0, 0);
+    for (uint32_t j0 = 0; j0 < sg.kin; j0 += KC) {
+      uint4 d[KC];
 #pragma unroll
-    for (int g = 0; g < KC; ++g)
-      d[g] = j0 + g < sg.kin ? ld16<NT>(u.in(sg, j0 + g)) : make_uint4(0, 0, 0, 0);
+      for (int g = 0; g < KC; ++g)
+        d[g] = j0 + g < sg.kin ? ld16<NT>(u.in(sg, j0 + g)) : make_uint4(0, 0, 0, 0);
 #pragma unroll
-    for (int g = 0; g < KC; ++g) {
-      a.x ^= d[g].x;
-      a.y ^= d[g].y;
-      a.z ^= d[g].z;
-      a.w ^= d[g].w;
+      for (int g = 0; g < KC; ++g) {
+        a.x ^= d[g].x;
+        a.y ^= d[g].y;
+        a.z ^= d[g].z;
+        a.w ^= d[g].w;
+      }
     }
   }
   if (!u.valid) return;
+  if (sg.probe == MEMO_EC_PROBE_READ) {
+    if (a.x == 0x2545f491u && a.y == ~a.z && a.w == 0x6c078965u) st16<NT>(u.out(sg, 0), a);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < R; ++i) {
     const uint32_t b = (uint32_t)i * 0x01010101u;

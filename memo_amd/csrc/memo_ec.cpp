@@ -1231,8 +1231,8 @@ int memo_ec_encode_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n, const
 }
 
 int memo_ec_stream_probe(memo_ec_ctx* c, int kin, int r, size_t S, size_t n, const uint8_t* in,
-                         uint8_t* out) {
-  if (!c) return MEMO_EC_EINVAL;
+                         uint8_t* out, int mode) {
+  if (!c || mode < MEMO_EC_PROBE_COPY || mode > MEMO_EC_PROBE_WRITE) return MEMO_EC_EINVAL;
   if (int rc = check_km(kin, r)) return rc;
   if (r == 0 || n == 0) return MEMO_EC_OK;
   if (S == 0 || S % 64 != 0 || !in || !out) return MEMO_EC_EINVAL;
@@ -1248,6 +1248,7 @@ int memo_ec_stream_probe(memo_ec_ctx* c, int kin, int r, size_t S, size_t n, con
                           nullptr, 0, KC, R);
     p.mode = MAC_PROBE;
     p.lds = 0;
+    p.seg.probe = (uint32_t)mode;
     std::vector<Plan> plans{p};
     if (int rc = launch_plans(c, plans, c->stream)) return rc;
   }

@@ -56,6 +56,7 @@ OPTIONS = {"rebuild_path": 1, "fused_max_bytes": 2, "zero_copy_bytes": 3, "pipe_
            "copy_threads": 5, "max_launch_tiles": 6, "xcd_min_tiles": 7, "decode_wide_max": 8,
            "decode_exact": 9, "decode_stage": 10}
 MAX_REBUILD_SEGMENTS = 256
+PROBE_MODES = {"copy": 0, "read": 1, "write": 2}  # memo_ec_probe_mode
 
 # The sources memo_ec_build_id() hashes, in its order (memo_amd/csrc/Makefile).
 _ROOT = os.path.dirname(_HERE)
@@ -122,7 +123,7 @@ def _lib():
         L.memo_ec_ctx_get_option.argtypes = [ctypes.c_void_p, c_int, ctypes.POINTER(ctypes.c_int64)]
         L.memo_ec_build_id.restype = ctypes.c_char_p
         L.memo_ec_device_identity.argtypes = [c_int, ctypes.c_char_p, _sz, ctypes.c_char_p, _sz]
-        L.memo_ec_stream_probe.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p]
+        L.memo_ec_stream_probe.argtypes = [ctypes.c_void_p, c_int, c_int, _sz, _sz, _u8p, _u8p, c_int]
         _LIB = L
     return _LIB
 
@@ -407,12 +408,13 @@ class Codec:
                                            lp or None, ul, _ptr(digest)[0]), "sha256")
         return digest
 
-    def stream_probe(self, kin, r, inp, out):
+    def stream_probe(self, kin, r, inp, out, mode="copy"):
         """memo_ec_stream_probe: the encode's traffic for (k, m) = (kin, r)
-        without the GF arithmetic (device tensors; asynchronous)."""
+        without the GF arithmetic (device tensors; asynchronous); mode
+        'copy' (loads and stores), 'read' or 'write' (one side alone)."""
         n, S = _infer_nS(inp, kin)
-        _check(_lib().memo_ec_stream_probe(self._ctx, kin, r, S, n, _ptr(inp)[0], _ptr(out)[0]),
-               "stream_probe")
+        _check(_lib().memo_ec_stream_probe(self._ctx, kin, r, S, n, _ptr(inp)[0], _ptr(out)[0],
+                                           PROBE_MODES[mode]), "stream_probe")
         return out
 
     def fill_blocks(self, seed, first_block, n, B, k, S, out):

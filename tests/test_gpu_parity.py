@@ -1095,6 +1095,16 @@ def test_stream_probe_bytes(codec, kin, r, B, n):
     acc = np.bitwise_xor.reduce(x.reshape(n, kin, S), axis=1)
     want = np.stack([acc ^ np.uint8(i) for i in range(r)], axis=1).reshape(n, r * S)
     assert np.array_equal(host(out), want)
+    # the one-sided modes run (read: out untouched for these inputs; write:
+    # every output byte written) and a bad mode is refused
+    codec.stream_probe(kin, r, dev(x), out, "read")
+    codec.synchronize()
+    assert np.array_equal(host(out), want)
+    codec.stream_probe(kin, r, dev(x), out, "write")
+    codec.synchronize()
+    assert not np.array_equal(host(out), want)
+    L = ec._lib()
+    assert L.memo_ec_stream_probe(codec._ctx, kin, r, S, n, out.data_ptr(), out.data_ptr(), 3) == -1
 
 
 def test_device_identity(codec):
