@@ -890,8 +890,12 @@ def pmc_small(args, result, local, world):
                         key = (int(md.group(1)), "decode rows")
                     else:
                         continue
-                    vals.setdefault(key, {}).setdefault((row.get("Dispatch_Id"), ), {})[
-                        row["Counter_Name"]] = float(row["Counter_Value"])
+                    dd = vals.setdefault(key, {}).setdefault((row.get("Dispatch_Id"), ), {})
+                    dd[row["Counter_Name"]] = float(row["Counter_Value"])
+                    try:
+                        dd["_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                    except (KeyError, ValueError):
+                        pass
     except (OSError, RuntimeError, subprocess.SubprocessError, KeyError, ValueError) as ex:
         result.setdefault("rebuild_small", {})["counters_note"] = "counter pass failed: %s" % str(ex)[:300]
         return
@@ -904,7 +908,10 @@ def pmc_small(args, result, local, world):
             return float(np.median(v)) if v else 0.0
         waves = med("SQ_WAVES") or 1.0
         cycles = med("GRBM_GUI_ACTIVE") / 8
+        ns = med("_ns")
         out = {"valu_busy": round(med("SQ_INSTS_VALU") * 2 / (1024 * cycles), 4) if cycles else None,
+               "clock_GHz": round(cycles / ns, 3) if ns else None,
+               "cycles_per_wave": round(4 * med("SQ_WAVE_CYCLES") / waves),
                "valu_per_wave": round(med("SQ_INSTS_VALU") / waves, 1),
                "salu_per_wave": round(med("SQ_INSTS_SALU") / waves, 1),
                "lds_per_wave": round(med("SQ_INSTS_LDS") / waves, 1),
@@ -920,7 +927,10 @@ def pmc_small(args, result, local, world):
             result["rebuild_small"][name].setdefault("counters", {})[kind] = summary(disp)
     result.setdefault("rebuild_small", {})["counters_source"] = (
         "rocprofv3 --pmc %s, one pass over a child run of the same 4 KiB lines (3 steps), per-dispatch "
-        "medians; valu_busy = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8)" % " ".join(SMALL_PMC))
+        "medians; valu_busy = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8); clock_GHz = "
+        "GRBM_GUI_ACTIVE / 8 / the dispatch's duration (counter passes serialise dispatches and run "
+        "a few % below the unprofiled clock); *_cycles_per_wave from the quad-cycle SQ counters" %
+        " ".join(SMALL_PMC))
 
 
 def merge_extras(result, extras):

