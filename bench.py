@@ -392,7 +392,7 @@ class HostStage:
         nb = (r1 - r0) * cols
         b = self.pinned.get(name)
         if b is None or b.numel() < nb:
-            b = t.empty(max(nb, self.chunk), dtype=t.uint8, pin_memory=True)
+            b = t.empty(max(nb, self.chunk), dtype=t.uint8, pin_memory=t.cuda.is_available())
             self.pinned[name] = b
         v = b[:nb].view(r1 - r0, cols)
         v.copy_(dev[r0:r1])
@@ -809,6 +809,8 @@ def pmc_traffic(args, result, local, world):
                         kd = kind(row.get("Kernel_Name", ""))
                         if kd:
                             vals.setdefault(kd, []).append(float(row["Counter_Value"]))
+            if not vals.get("encode"):
+                raise RuntimeError("no encode kernel in the %s counter files" % counter)
             per[counter] = vals
     except (OSError, RuntimeError, subprocess.SubprocessError, KeyError, ValueError) as ex:
         for key in ("roofline", "roofline_rebuild"):
@@ -896,6 +898,8 @@ def pmc_small(args, result, local, world):
                         dd["_ns"] = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
                     except (KeyError, ValueError):
                         pass
+        if not vals:
+            raise RuntimeError("no codec kernel in the counter files")
     except (OSError, RuntimeError, subprocess.SubprocessError, KeyError, ValueError) as ex:
         result.setdefault("rebuild_small", {})["counters_note"] = "counter pass failed: %s" % str(ex)[:300]
         return
@@ -929,7 +933,7 @@ def pmc_small(args, result, local, world):
         "rocprofv3 --pmc %s, one pass over a child run of the same 4 KiB lines (3 steps), per-dispatch "
         "medians; valu_busy = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8); clock_GHz = "
         "GRBM_GUI_ACTIVE / 8 / the dispatch's duration (counter passes serialise dispatches and run "
-        "a few % below the unprofiled clock); *_cycles_per_wave from the quad-cycle SQ counters" %
+        "a few %% below the unprofiled clock); *_cycles_per_wave from the quad-cycle SQ counters" %
         " ".join(SMALL_PMC))
 
 

@@ -304,3 +304,127 @@ def test_bench_n2_line_is_self_sufficient():
     assert res["roofline"]["traffic"] > 0 and res["roofline"]["traffic_ratio"] < 1.5, res["roofline"]
     assert res["roofline_rebuild"]["traffic"] > 0
     assert res["build_matches_sources"]
+
+
+def _fake_rocprof(monkeypatch, rows_by_counter):
+    """subprocess.run stand-in for the bench's rocprofv3 child runs: writes
+    a counter_collection.csv with the given rows into the -d directory."""
+    import csv
+    import subprocess
+
+    class R:
+        returncode = 0
+        stderr = b""
+
+    def run(cmd, **kw):
+        d = cmd[cmd.index("-d") + 1]
+        os.makedirs(os.path.join(d, "host"), exist_ok=True)
+        pmc = cmd[cmd.index("--pmc") + 1:cmd.index("-d")]
+        with open(os.path.join(d, "host", "x_counter_collection.csv"), "w", newline="") as f:
+            w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value",
+                                              "Start_Timestamp", "End_Timestamp"])
+            w.writeheader()
+            for r in rows_by_counter:
+                if r["Counter_Name"] in pmc:
+                    w.writerow(r)
+        return R()
+    monkeypatch.setattr(subprocess, "run", run)
+
+
+def test_counter_passes_fold_into_the_line(monkeypatch):
+    """pmc_traffic and pmc_small (run after the timed steps as rocprofv3
+    child processes) parse the counter files into roofline.traffic and the
+    4 KiB lines' counters; a failed pass leaves a note, never a crash."""
+    import bench
+    args = bench.parse(["--gpus", "1"])
+    S, n = 104896, 4096
+    enc = "void memo_ec::gf_mac_kernel<10, 4, true, false>(memo_ec::MacLaunch)"
+    reb = "void memo_ec::gf_mac_kernel<10, 4, true, true>(memo_ec::MacLaunch)"
+    rows = []
+    for disp, name, fetch, write in [(1, enc, 2.9e6, 1.7e6), (2, reb, 2.95e6, 1.7e6)]:
+        rows += [{"Dispatch_Id": disp, "Kernel_Name": name, "Counter_Name": "FETCH_SIZE",
+                  "Counter_Value": fetch, "Start_Timestamp": 0, "End_Timestamp": 1},
+                 {"Dispatch_Id": disp, "Kernel_Name": name, "Counter_Name": "WRITE_SIZE",
+                  "Counter_Value": write, "Start_Timestamp": 0, "End_Timestamp": 1}]
+    k16e = "void memo_ec::gf_mac_kernel<16, 4, true, false>(memo_ec::MacLaunch)"
+    k16r = "void memo_ec::gf_mac_kernel<16, 4, true, true>(memo_ec::MacLaunch)"
+    dec = "void memo_ec::decode_rows_k_kernel<16, 4>(memo_ec::DecodeLaunch)"
+    for disp, name in [(10, k16e), (11, dec), (12, k16r)]:
+        for c, v in [("SQ_INSTS_VALU", 4.3e8), ("SQ_INSTS_SALU", 2.2e7), ("SQ_INSTS_LDS", 2.6e7),
+                     ("SQ_WAVES", 262144), ("SQ_ACTIVE_INST_ANY", 4.9e8), ("SQ_WAIT_INST_ANY", 4.6e8),
+                     ("SQ_WAIT_ANY", 2.8e8), ("SQ_WAVE_CYCLES", 1.38e9), ("GRBM_GUI_ACTIVE", 1.57e7)]:
+            rows.append({"Dispatch_Id": disp, "Kernel_Name": name, "Counter_Name": c, "Counter_Value": v,
+                         "Start_Timestamp": 1000, "End_Timestamp": 1000 + 906000})
+    _fake_rocprof(monkeypatch, rows)
+    res = {"build_id": "x" * 64,
+           "roofline": {"bytes_per_launch": 14 * S * n}, "roofline_rebuild": {"bytes_per_launch": 14 * S * n},
+           "rebuild_small": {"RS(16,4)": {"frac": 0.65}, "RS(10,4)": {"frac": 0.71}}}
+    bench.pmc_traffic(args, res, 0, 1)
+    assert res["roofline"]["traffic"] == int(round((2 * 2.9e6 + 1.7e6) * 1024))
+    assert res["roofline_rebuild"]["traffic"] > 0 and "traffic_source" in res["roofline_rebuild"]
+    bench.pmc_small(args, res, 0, 1)
+    c = res["rebuild_small"]["RS(16,4)"]["counters"]
+    assert set(c) == {"encode MAC", "rebuild MAC", "decode rows"}
+    assert c["rebuild MAC"]["valu_busy"] == round(4.3e8 * 2 / (1024 * 1.57e7 / 8), 4)
+    assert c["encode MAC"]["clock_GHz"] == round(1.57e7 / 8 / 906000, 3)
+    assert c["encode MAC"]["valu_per_wave"] == round(4.3e8 / 262144, 1)
+    assert "counters_source" in res["rebuild_small"]
+    # a pass that produces nothing: a note in the line, no exception
+    _fake_rocprof(monkeypatch, [])
+    res2 = {"build_id": "x" * 64, "roofline": {"bytes_per_launch": 1}, "rebuild_small": {"RS(16,4)": {}}}
+    bench.pmc_small(args, res2, 0, 1)
+    assert "counters_note" in res2["rebuild_small"]
+    bench.pmc_traffic(args, res2, 0, 1)
+    assert res2["roofline"]["traffic"] is None and "traffic_note" in res2["roofline"]
+
+
+def test_whole_batch_checks_catch_one_byte():
+    """verify_encode / verify_rebuild (the bench line's whole-batch oracle
+    comparison) stream a batch through small staging chunks and report one
+    flipped byte anywhere in it (CPU tensors stand in for device ones)."""
+    import torch
+    import bench
+    from oracle import oracle as O
+    k, m, B, n, e = 4, 2, 5000, 37, 2
+    S = O.shard_size(B, k)
+    data = O.fill_blocks(SEED, 0, n, B, k, S)
+    par = O.encode(k, m, S, data)
+    stage = bench.HostStage(torch, chunk_bytes=5 * (k + m) * S)  # several chunks
+    d, p = torch.from_numpy(data.copy()), torch.from_numpy(par.copy())
+    assert bench.verify_encode(stage, k, m, S, d, p, 2)["bit_exact"]
+    p[n - 1, m * S - 1] ^= 1
+    v = bench.verify_encode(stage, k, m, S, d, p, 2)
+    assert not v["bit_exact"] and v["blocks"] == n and v["bytes_compared"] == n * m * S
+    s_idx, l_idx = O.erasures(SEED, 0, n, k, m, e)
+    surv = torch.from_numpy(O.gather(k, m, S, data, par, s_idx))
+    out = torch.from_numpy(O.gather(k, m, S, data, par, l_idx))
+    assert bench.verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, 2)["bit_exact"]
+    out[17, 5] ^= 0x80
+    assert not bench.verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, 2)["bit_exact"]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(600)
+def test_bench_default_line_runs_every_leg():
+    """The driver's own command shape at N = 1 (fewer steps, a short CPU
+    sample): the line carries the whole-batch oracle comparison of C2, C3,
+    the 4 KiB rebuilds and C5, the achievable-rate probe, the 4 KiB counter
+    summary, counter traffic, the CPU baseline and the device identity."""
+    import subprocess
+    import sys
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5",
+                        "--warmup", "2", "--cpu-seconds", "1"],
+                       capture_output=True, text=True, timeout=560, cwd=ROOT)
+    res = _bench_json(r)
+    assert res["oracle_bit_exact"] is True
+    assert set(res["oracle_parity"]) == {"C2_encode", "C3_rebuild"}
+    for name in ("RS(10,4)", "RS(16,4)"):
+        sm = res["rebuild_small"][name]
+        assert sm["oracle"]["bit_exact"] and sm["uniform_pattern"]["bit_exact"]
+        assert 0 < sm["frac_of_achievable"] <= 1.05
+        assert set(sm["counters"]) == {"encode MAC", "rebuild MAC", "decode rows"}, res["rebuild_small"]
+    assert res["c5_mixed"]["oracle_bit_exact"] and len(res["c5_mixed"]["groups"]) == 12
+    assert 0 < res["roofline"]["frac_of_achievable"] <= 1.0
+    assert res["roofline"]["traffic_ratio"] < 1.1
+    assert res["cpu_baseline"]["bit_exact_vs_gpu"] and res["c1"]["bit_exact"]
+    assert res["ranks"]["per_gpu"][0]["uuid"] and res["build_matches_sources"]
