@@ -869,8 +869,9 @@ def pmc_small(args, result, local, world):
     if world > 1 and not args.same_device:
         var, dev = _visible_device(local)
         env[var] = dev
-    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--small-only", "--steps", "3",
-             "--warmup", "1", "--settle-ms", "0"]
+    # clocks settled first (150 ms of untimed steps), as the timed lines are
+    child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--small-only", "--steps", "4",
+             "--warmup", "2", "--settle-ms", "150"]
     tmp = tempfile.mkdtemp(prefix="memo_pmc_small_", dir=os.environ.get("TMPDIR", "/tmp"))
     vals = {}
     try:
@@ -930,7 +931,8 @@ def pmc_small(args, result, local, world):
         if name and name in result.get("rebuild_small", {}):
             result["rebuild_small"][name].setdefault("counters", {})[kind] = summary(disp)
     result.setdefault("rebuild_small", {})["counters_source"] = (
-        "rocprofv3 --pmc %s, one pass over a child run of the same 4 KiB lines (3 steps), per-dispatch "
+        "rocprofv3 --pmc %s, one pass over a child run of the same 4 KiB lines (4 steps after 150 ms of "
+        "untimed ones), per-dispatch "
         "medians; valu_busy = SQ_INSTS_VALU * 2 / (1024 SIMDs * GRBM_GUI_ACTIVE / 8); clock_GHz = "
         "GRBM_GUI_ACTIVE / 8 / the dispatch's duration (counter passes serialise dispatches and run "
         "a few %% below the unprofiled clock); *_cycles_per_wave from the quad-cycle SQ counters" %
