@@ -59,6 +59,12 @@ def test_error_codes_and_limits():
     assert L.memo_ec_encode_batch(None, 10, 4, 64, 1, None, None, 2) == -1
     assert L.memo_ec_rebuild_segments(None, 0, None, 2) == -1
     assert L.memo_ec_ctx_set_option(None, 1, 0) == -1
+    assert L.memo_ec_stream_probe(None, 10, 4, 64, 1, None, None, 0) == -1
+    buf = ctypes.create_string_buffer(64)
+    assert L.memo_ec_device_identity(0, buf, 8, buf, 64) == -1       # short bus-id buffer
+    assert L.memo_ec_device_identity(0, buf, 64, buf, 16) == -1      # short UUID buffer
+    if L.memo_ec_device_count() == 0:                                # no GPU here: no device 0
+        assert L.memo_ec_device_identity(0, buf, 64, buf, 64) == -5
 
 
 def test_build_id_matches_sources():
