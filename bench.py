@@ -84,6 +84,8 @@ def parse(argv=None):
                     help="skip the whole-batch oracle comparisons after the timed steps")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 mixed-geometry point")
     ap.add_argument("--c5-gib", type=float, default=4.0, help="payload GiB of the C5 mixed point")
+    ap.add_argument("--no-plugin", action="store_true",
+                    help="skip the plugin-level lines (host/_build/bench_plugin child runs)")
     ap.add_argument("--rank-timeout", type=float, default=600.0,
                     help="seconds a rank may take (launcher kill bound, gloo collective timeout)")
     return ap.parse_args(argv)
@@ -844,6 +846,42 @@ def pmc_traffic(args, result, local, world):
         result["roofline_rebuild"]["traffic_source"] = src
 
 
+PLUGIN_BIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "host", "_build", "bench_plugin")
+# (blocks, block bytes): the 4 KiB-block point of SURVEY.md 8(d) and 1 MiB
+# blocks, through the whole consensus (place, silo writes, multi-fetch,
+# eviction + repair) beside replication; a few seconds each.
+PLUGIN_SIZES = [(16384, 4096), (512, 1 << 20)]
+PLUGIN_KEYS = ("store_GiBs", "fetch_GiBs", "degraded_fetch_GiBs", "repair_GiBs")
+
+
+def plugin_lines(binary=PLUGIN_BIN, sizes=PLUGIN_SIZES, timeout=240):
+    """The plugin level (host/erasure_consensus.cc, the drop-in for the
+    reference's Consensus, src/memo/model/doughnut/Consensus.hh:24-174): child runs
+    of host/tests/bench_plugin.cc, each on in-process memory-silo nodes, which
+    exit non-zero unless every healthy, degraded and post-repair fetch returns
+    bytes whose SHA-256 matches the block's CHB address and nothing is left
+    unrecoverable.  Host-bound (the place step and silo copies), not a kernel
+    roofline line; it runs after the timed region."""
+    import subprocess
+    out = {}
+    for nb, bb in sizes:
+        key = "%dx%d" % (nb, bb)
+        try:
+            r = subprocess.run([binary, str(nb), str(bb)], stdout=subprocess.PIPE,
+                               stderr=subprocess.PIPE, timeout=timeout)
+            line = r.stdout.decode(errors="replace").strip().splitlines()
+            d = json.loads(line[-1]) if line else {}
+            er, rp = d.get("erasure", {}), d.get("replication", {})
+            row = {"ok": r.returncode == 0 and all(x in er for x in PLUGIN_KEYS),
+                   "erasure": er, "replication": rp}
+            if not row["ok"]:
+                row["note"] = "rc %d: %s" % (r.returncode, r.stderr.decode(errors="replace")[-300:])
+        except (OSError, subprocess.SubprocessError, ValueError, IndexError) as ex:
+            row = {"ok": False, "note": str(ex)[:300]}
+        out[key] = row
+    return out
+
+
 SMALL_PMC = ["SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES", "SQ_ACTIVE_INST_ANY",
              "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"]
 
@@ -1244,6 +1282,9 @@ def main():
             pmc_traffic(args, result, local, world)
             if "rebuild_small" in result:
                 pmc_small(args, result, local, world)
+        if not args.no_plugin and world == 1:
+            log("plugin lines")
+            result["plugin"] = plugin_lines()
         if args.sha:
             result["sha256"] = sha_lines(torch, codec, stream, data, n, B)
         if args.sweep and world == 1:

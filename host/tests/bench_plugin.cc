@@ -129,6 +129,11 @@ int main(int argc, char** argv) {
   t = now();
   const auto rep = ec.repair();
   const double t_repair = now() - t;
+  // every block reads back (CHB address re-checked on the reassembled
+  // bytes) from the repaired placement, the evicted nodes gone
+  ok = 0;
+  ec.fetch(addrs, check);
+  const bool repaired_ok = ok == nb;
 
   // ---- replication (memo's path today): factor full copies
   Net rn(N);
@@ -151,15 +156,16 @@ int main(int argc, char** argv) {
       "\"fetch_ok\": %s, \"degraded_fetch_GiBs\": %.2f, \"degraded_fetch_cold_GiBs\": %.2f, "
       "\"degraded_ok\": %s, "
       "\"degraded_codec_calls\": %llu, \"repair_GiBs\": %.2f, \"repaired_blocks\": %zu, "
-      "\"repair_codec_calls\": %zu, \"unrecoverable\": %zu, \"stored_bytes_per_byte\": %.2f}, "
+      "\"repair_codec_calls\": %zu, \"unrecoverable\": %zu, \"fetch_after_repair_ok\": %s, "
+      "\"stored_bytes_per_byte\": %.2f}, "
       "\"replication\": {\"factor\": %d, \"store_GiBs\": %.2f, \"fetch_GiBs\": %.2f, "
       "\"fetch_ok\": %s, \"stored_bytes_per_byte\": %d}}\n",
       nb, B, N, gib(total, t_chb), k, m, gib((nb - half) * B, t_store), gib(half * B, t_store_cold),
       gib(total, t_fetch), fetch_ok ? "true" : "false", gib(total, t_degraded),
       gib(total, t_degraded_cold), degraded_ok ? "true" : "false",
       (unsigned long long)degraded_calls, gib(rep.blocks_repaired * B, t_repair),
-      rep.blocks_repaired, rep.codec_calls, rep.unrecoverable,
+      rep.blocks_repaired, rep.codec_calls, rep.unrecoverable, repaired_ok ? "true" : "false",
       (double)(k + m) * memo_ec_shard_size(B, k) / B, factor, gib(total, t_rstore),
       gib(total, t_rfetch), rfetch_ok ? "true" : "false", factor);
-  return fetch_ok && degraded_ok && rfetch_ok && rep.unrecoverable == 0 ? 0 : 1;
+  return fetch_ok && degraded_ok && rfetch_ok && repaired_ok && rep.unrecoverable == 0 ? 0 : 1;
 }

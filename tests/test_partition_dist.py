@@ -1,6 +1,7 @@
 """Multi-rank path on CPU (gloo, world_size 2): block-index partition is
 disjoint and complete, per-rank synthetic inputs equal the single-rank
 global batch, and the job time is the max over ranks."""
+import json
 import os
 import socket
 
@@ -409,7 +410,8 @@ def test_bench_default_line_runs_every_leg():
     """The driver's own command shape at N = 1 (fewer steps, a short CPU
     sample): the line carries the whole-batch oracle comparison of C2, C3,
     the 4 KiB rebuilds and C5, the achievable-rate probe, the 4 KiB counter
-    summary, counter traffic, the CPU baseline and the device identity."""
+    summary, counter traffic, the CPU baseline, the device identity and the
+    plugin-level lines."""
     import subprocess
     import sys
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5",
@@ -428,3 +430,26 @@ def test_bench_default_line_runs_every_leg():
     assert res["roofline"]["traffic_ratio"] < 1.1
     assert res["cpu_baseline"]["bit_exact_vs_gpu"] and res["c1"]["bit_exact"]
     assert res["ranks"]["per_gpu"][0]["uuid"] and res["build_matches_sources"]
+    for key, pl in res["plugin"].items():
+        assert pl["ok"] and pl["erasure"]["fetch_after_repair_ok"], (key, pl)
+        assert pl["erasure"]["unrecoverable"] == 0 and pl["erasure"]["degraded_codec_calls"] >= 1
+
+
+def test_plugin_lines_parse_and_flag_failures(tmp_path):
+    """bench.py's plugin leg on a stand-in binary (no GPU): a clean run is
+    kept whole, a non-zero exit or a missing rate marks the row not ok with
+    the child's stderr, and a missing binary is a note, not a crash."""
+    import bench
+    line = json.dumps({"workload": "x", "erasure": {k: 1.0 for k in bench.PLUGIN_KEYS} | {
+        "fetch_after_repair_ok": True, "unrecoverable": 0}, "replication": {"fetch_GiBs": 2.0}})
+    fake = tmp_path / "bench_plugin"
+    fake.write_text("#!/bin/sh\n[ \"$1\" = 3 ] && { echo oops >&2; echo '%s'; exit 1; }\n"
+                    "[ \"$1\" = 5 ] && { echo '{\"erasure\": {}}'; exit 0; }\necho '%s'\n" % (line, line))
+    fake.chmod(0o755)
+    out = bench.plugin_lines(str(fake), [(2, 4096), (3, 4096), (5, 64)], timeout=30)
+    assert out["2x4096"]["ok"] and out["2x4096"]["erasure"]["fetch_after_repair_ok"]
+    assert out["2x4096"]["replication"]["fetch_GiBs"] == 2.0
+    assert not out["3x4096"]["ok"] and "oops" in out["3x4096"]["note"]
+    assert not out["5x64"]["ok"]
+    gone = bench.plugin_lines(str(tmp_path / "missing"), [(1, 1)], timeout=30)
+    assert not gone["1x1"]["ok"] and gone["1x1"]["note"]
