@@ -7,7 +7,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <optional>
 #include <set>
+#include <unordered_map>
 
 namespace memo_host {
 
@@ -328,7 +330,9 @@ uint32_t shard_crc(const uint8_t* wire, size_t S) {
 }
 }  // namespace
 
-Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
+Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) { return encode_shard(h, payload, h.index); }
+
+Buffer encode_shard(const ShardHeader& h, const uint8_t* payload, int index) {
   if (h.salt.size() > 32) throw Error("shard: salt longer than 32 bytes");
   Buffer w;
   w.reserve(ShardHeader::kSize + h.shard_size);
@@ -338,7 +342,7 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) {
   w[4] = ShardHeader::kVersion;
   w[5] = h.k;
   w[6] = h.m;
-  w[7] = h.index;
+  w[7] = (uint8_t)index;
   std::memcpy(w.data() + 8, &h.block_size, 8);
   std::memcpy(w.data() + 16, &h.shard_size, 8);
   std::memcpy(w.data() + 24, h.address.value.data(), 32);
@@ -649,7 +653,7 @@ void NodeIndex::update(const Address& block, const std::vector<Address>& old_h,
   }
 }
 
-void NodeIndex::update_many(const std::vector<Change>& changes) {
+void NodeIndex::update_many(const std::vector<Change>& changes, ThreadPool* pool) {
   auto has = [](const std::vector<Address>& v, const Address& x) {
     return std::find(v.begin(), v.end(), x) != v.end();
   };
@@ -674,8 +678,15 @@ void NodeIndex::update_many(const std::vector<Change>& changes) {
         ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
     }
   }
-  for (size_t si = 0; si < kStripes; ++si) {
-    if (ops[si].empty()) continue;
+  std::vector<size_t> busy;
+  size_t nops = 0;
+  for (size_t si = 0; si < kStripes; ++si)
+    if (!ops[si].empty()) {
+      busy.push_back(si);
+      nops += ops[si].size();
+    }
+  auto apply = [&](size_t t) {
+    const size_t si = busy[t];
     Stripe& s = st_[si];
     std::lock_guard<std::mutex> g(s.mu);
     for (auto& [h, b, add] : ops[si]) {
@@ -688,7 +699,10 @@ void NodeIndex::update_many(const std::vector<Change>& changes) {
         if (it->second.empty()) s.m.erase(it);
       }
     }
-  }
+  };
+  if (pool && busy.size() > 1 && nops >= 256) pool->parallel_for(busy.size(), apply);
+  else
+    for (size_t t = 0; t < busy.size(); ++t) apply(t);
 }
 
 std::vector<Address> NodeIndex::blocks(const Address& node) const {
@@ -770,64 +784,102 @@ void ErasureConsensus::batcher_loop() {
   }
 }
 
-// Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360).
-void ErasureConsensus::place(const Block& b, const uint8_t* parity, size_t pstride,
-                             const uint8_t* data, size_t dstride, bool parallel, Placed* defer) {
-  const int total = o_.k + o_.m;
+// Send shard i to owner i (send_immutable_block's fan-out, Paxos.cc:324-360):
+// a batch of one, recorded at once.
+void ErasureConsensus::place(const Block& b, const uint8_t* parity) {
   const size_t S = memo_ec_shard_size(b.data.size(), o_.k);
-  Buffer own;
-  if (!data) {  // the block's own shards, zero-padded
-    own = padded(b, S);
-    data = own.data();
-    dstride = S;
+  const Buffer own = padded(b, S);  // the block's own shards, zero-padded
+  std::vector<Placed> placed(1);
+  const std::exception_ptr err = place_batch({&b}, own.data(), parity, S, placed);
+  commit_placements(placed);
+  if (err) std::rethrow_exception(err);
+}
+
+std::exception_ptr ErasureConsensus::place_batch(const std::vector<const Block*>& bs, const uint8_t* data,
+                                                 const uint8_t* parity, size_t S,
+                                                 std::vector<Placed>& placed) {
+  const int k = o_.k, m = o_.m, total = k + m;
+  const size_t n = bs.size();
+  PhaseTimer tm("place_batch");
+  std::vector<std::vector<std::shared_ptr<Node>>> owners(n);
+  std::vector<std::optional<ShardKeys>> keys(n);
+  std::vector<ShardHeader> hdr(n);
+  pool_.parallel_for(n, [&](size_t i) {
+    const Block& b = *bs[i];
+    owners[i] = overlay_.allocate(b.address, total);
+    keys[i].emplace(b.address);
+    Placement pl;
+    pl.B = b.data.size();
+    pl.salt = b.salt;
+    pl.owner = b.owner;
+    hdr[i] = header_of(b.address, pl, 0);
+  });
+  tm.lap("owners");
+  // an owner's shards as runs of at most `run` (a few tasks per owner keep
+  // every pool thread busy; each run still meets its node alone)
+  std::unordered_map<Node*, std::vector<uint32_t>> by_node;
+  size_t entries = 0;
+  for (size_t i = 0; i < n; ++i)
+    if ((int)owners[i].size() >= k)
+      for (size_t j = 0; j < owners[i].size(); ++j) {
+        by_node[owners[i][j].get()].push_back((uint32_t)(i * total + j));
+        ++entries;
+      }
+  const size_t run = std::max<size_t>(32, entries / (4 * std::max<size_t>(1, pool_.size())) + 1);
+  std::vector<std::pair<Node*, std::pair<const uint32_t*, size_t>>> tasks;
+  for (auto& [nd, v] : by_node)
+    for (size_t o = 0; o < v.size(); o += run) tasks.push_back({nd, {v.data() + o, std::min(run, v.size() - o)}});
+  std::vector<uint8_t> ok(n * total, 0);
+  tm.lap("group");
+  pool_.parallel_for(tasks.size(), [&](size_t t) {
+    Node* nd = tasks[t].first;
+    const auto [e0, ne] = tasks[t].second;
+    for (size_t x = 0; x < ne; ++x) {
+      const uint32_t e = e0[x];
+      const size_t i = e / total;
+      const int j = (int)(e % total);
+      const uint8_t* p = j < k ? data + (i * k + j) * S : parity + (i * m + (j - k)) * S;
+      try {
+        nd->store((*keys[i])(j), encode_shard(hdr[i], p, j));
+        ok[e] = 1;
+      } catch (Unavailable&) {
+      }
+    }
+  });
+  tm.lap("stores");
+  std::exception_ptr err;
+  size_t stored = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const Block& b = *bs[i];
+    if ((int)owners[i].size() < k) {
+      if (!err)
+        err = std::make_exception_ptr(TooFewPeers("erasure: " + std::to_string(owners[i].size()) +
+                                                  " reachable owners, need " + std::to_string(k)));
+      continue;
+    }
+    Placed& d = placed[i];
+    d.a = b.address;
+    d.pl.B = b.data.size();
+    d.pl.salt = b.salt;
+    d.pl.owner = b.owner;
+    d.pl.holder.assign(total, Address());
+    int reached = 0;
+    for (size_t j = 0; j < owners[i].size(); ++j)
+      if (ok[i * total + j]) {
+        d.pl.holder[j] = owners[i][j]->id;
+        ++reached;
+      }
+    d.set = true;
+    if (reached < k) {
+      if (!err)
+        err = std::make_exception_ptr(TooFewPeers("erasure: stored " + std::to_string(reached) +
+                                                  " shards, need " + std::to_string(k)));
+    } else {
+      ++stored;
+    }
   }
-  auto owners = overlay_.allocate(b.address, total);
-  if ((int)owners.size() < o_.k)
-    throw TooFewPeers("erasure: " + std::to_string(owners.size()) + " reachable owners, need " +
-                      std::to_string(o_.k));
-  Placement pl;
-  pl.B = b.data.size();
-  pl.salt = b.salt;
-  pl.owner = b.owner;
-  pl.holder.assign(total, Address());
-  std::vector<int> ok(total, 0);
-  const ShardKeys keys(b.address);
-  auto put = [&](size_t i) {
-    const ShardHeader h = header_of(b.address, pl, (int)i);
-    const uint8_t* p = i < (size_t)o_.k ? data + i * dstride : parity + (i - o_.k) * pstride;
-    try {
-      owners[i]->store(keys((int)i), encode_shard(h, p));
-      ok[i] = 1;
-    } catch (Unavailable&) {
-    }
-  };
-  if (parallel) pool_.parallel_for(owners.size(), put);
-  else
-    for (size_t i = 0; i < owners.size(); ++i) put(i);
-  int reached = 0;
-  for (size_t i = 0; i < owners.size(); ++i)
-    if (ok[i]) {
-      pl.holder[i] = owners[i]->id;
-      ++reached;
-    }
-  if (defer) {
-    defer->a = b.address;
-    defer->pl = std::move(pl);
-    defer->set = true;
-  } else {
-    const std::vector<Address> holders = pl.holder;
-    std::vector<Address> old;
-    {
-      std::unique_lock<std::shared_mutex> g(index_mu_);
-      old = swap_placement_locked(b.address, std::move(pl));
-    }
-    nodes_.update(b.address, old, holders);
-    if (o_.auto_expand && reached >= o_.k && reached < total) post(kUnderPlaced, b.address);
-  }
-  if (reached < o_.k)
-    throw TooFewPeers("erasure: stored " + std::to_string(reached) + " shards, need " +
-                      std::to_string(o_.k));
-  ++stored_;
+  stored_ += stored;
+  return err;
 }
 
 void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
@@ -848,7 +900,7 @@ void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
       ch.push_back(std::move(c));
     }
   }
-  nodes_.update_many(ch);
+  nodes_.update_many(ch, &pool_);
   if (o_.auto_expand)
     for (auto& a : under) post(kUnderPlaced, a);
 }
@@ -864,7 +916,7 @@ void ErasureConsensus::_store(const Block& b, StoreMode mode) {
   }
   bcv_.notify_all();
   const Buffer parity = fut.get();
-  place(b, parity.data(), memo_ec_shard_size(b.data.size(), o_.k), nullptr, 0);
+  place(b, parity.data());
 }
 
 void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
@@ -909,15 +961,7 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
       // the shards go out on the pool; the batch's placements then enter
       // the index under one lock (also when some block fell short)
       std::vector<Placed> placed(n);
-      std::exception_ptr err;
-      try {
-        pool_.parallel_for(n, [&](size_t i) {
-          place(*g.second[i], parity.data() + i * o_.m * S, S, data.data() + i * o_.k * S, S,
-                /*parallel=*/false, &placed[i]);  // already on the pool
-        });
-      } catch (...) {
-        err = std::current_exception();
-      }
+      std::exception_ptr err = place_batch(g.second, data.data(), parity.data(), S, placed);
       tm.lap("place");
       commit_placements(placed);
       tm.lap("index");
@@ -1693,7 +1737,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
           ch.push_back(std::move(c));
         }
       }
-      nodes_.update_many(ch);
+      nodes_.update_many(ch, &pool_);
       tm.lap("index");
       for (size_t bi = 0; bi < n; ++bi) {
         Todo& x = *rb.grp->items[rb.b0 + bi];

@@ -175,6 +175,9 @@ struct ShardHeader {
   }
 };
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
+// encode_shard with `index` in place of h.index (one header per block shared
+// by the threads framing its shards).
+Buffer encode_shard(const ShardHeader& h, const uint8_t* payload, int index);
 // Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
 // payload length, CRC32C over header and payload); throws ValidationFailed.
 ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
@@ -204,6 +207,7 @@ class ThreadPool {
   ~ThreadPool();
   // Runs fn(0..n-1) on the pool and waits; rethrows the first exception.
   void parallel_for(size_t n, const std::function<void(size_t)>& fn);
+  size_t size() const { return ts_.size(); }
 
  private:
   void worker();
@@ -229,14 +233,15 @@ class NodeIndex {
     Address block;
     std::vector<Address> old_h, new_h;
   };
-  // update() for many blocks, each stripe locked once
-  void update_many(const std::vector<Change>& changes);
+  // update() for many blocks, each stripe locked once; with a pool, the
+  // stripes in parallel (a batch of 256 4 KiB blocks is ~3600 set inserts)
+  void update_many(const std::vector<Change>& changes, ThreadPool* pool = nullptr);
   std::vector<Address> blocks(const Address& node) const;
   size_t count(const Address& node) const;
 
  private:
   static constexpr size_t kStripes = 32;
-  struct Stripe {
+  struct alignas(64) Stripe {
     mutable std::mutex mu;
     std::unordered_map<Address, std::unordered_set<Address, AddressHash>, AddressHash> m;
   };
@@ -374,15 +379,18 @@ class ErasureConsensus : public StackedConsensus {
                                   size_t stride);
   Buffer padded(const Block& b, size_t S) const;
   ShardHeader header_of(const Address& a, const Placement& pl, int index) const;
-  // parallel = false stores the shards one by one (callers on the pool).
-  // Shard i of b to owner i: data shard j at data + j*dstride (nullptr: b's
-  // own zero-padded payload), parity shard r at parity + r*pstride.
-  // defer: the placement is left in *defer for commit_placements (a batch
-  // of blocks then takes the index lock once) instead of recorded here.
+  // The shards of b (its own payload, zero-padded, and m x S parity) to its
+  // k + m owners, the placement recorded; TooFewPeers below k.
   struct Placed;
-  void place(const Block& b, const uint8_t* parity, size_t pstride, const uint8_t* data,
-             size_t dstride, bool parallel = true, Placed* defer = nullptr);
+  void place(const Block& b, const uint8_t* parity);
   void commit_placements(std::vector<Placed>& placed);
+  // place(..., defer) for a batch of blocks with their shards in S-byte
+  // slots (block i's data shard j at data + (i*k + j)*S, parity shard r at
+  // parity + (i*m + r)*S), the shards grouped by owner so that one pool task
+  // stores an owner's run of shards.  Every block is tried; returns the
+  // first failure (TooFewPeers) or null.
+  std::exception_ptr place_batch(const std::vector<const Block*>& bs, const uint8_t* data,
+                                 const uint8_t* parity, size_t S, std::vector<Placed>& placed);
   void batcher_loop();
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true);

@@ -218,7 +218,7 @@ class Silo {
   virtual int _erase(const Key& k) = 0;
   virtual std::vector<Key> _list() = 0;
   int64_t capacity_;
-  std::atomic<int64_t> usage_{0};
+  alignas(64) std::atomic<int64_t> usage_{0};  // written by every store thread
 };
 
 // silo::Memory (src/memo/silo/Memory.hh:10-61): the in-memory test silo.
@@ -243,7 +243,7 @@ class MemorySilo : public Silo {
   // the reference's Memory silo (src/memo/silo/Memory.hh:15), in stripes
   // with a lock each (the reference's silo serves one reactor thread; this
   // one serves a pool).
-  struct Stripe {
+  struct alignas(64) Stripe {
     mutable std::mutex mu;
     std::unordered_map<Key, std::shared_ptr<const Buffer>, AddressHash> blocks;
   };
@@ -286,9 +286,12 @@ struct Node {
   std::unique_ptr<Silo> silo;
   std::atomic<bool> up{true};
   std::atomic<bool> evicted{false};
-  std::atomic<int64_t> stores{0}, fetches{0};
   // store barrier (tests/doughnut.cc:1048-1163 instrumented Local)
   std::atomic<bool> fail_stores{false};
+  // counters written by every store / fetch thread: lines of their own, off
+  // the flags above that every operation reads
+  alignas(64) std::atomic<int64_t> stores{0};
+  alignas(64) std::atomic<int64_t> fetches{0};
 
   void store(const Key& k, const Buffer& v);
   void store(const Key& k, Buffer&& v);
