@@ -657,48 +657,59 @@ void NodeIndex::update_many(const std::vector<Change>& changes, ThreadPool* pool
   auto has = [](const std::vector<Address>& v, const Address& x) {
     return std::find(v.begin(), v.end(), x) != v.end();
   };
-  // (holder, block, add?) per stripe
-  std::array<std::vector<std::tuple<const Address*, const Address*, bool>>, kStripes> ops;
-  for (const Change& c : changes) {
-    // holders that stayed in place need no membership test (a repair moves
-    // e of k + m)
-    auto same_at = [&](const std::vector<Address>& v, size_t i, const Address& h) {
-      return i < v.size() && v[i] == h;
-    };
-    for (size_t i = 0; i < c.old_h.size(); ++i) {
-      const Address& h = c.old_h[i];
-      if (!h || same_at(c.new_h, i, h) || has(c.new_h, h) ||
-          std::find(c.old_h.begin(), c.old_h.begin() + i, h) != c.old_h.begin() + i)
-        continue;
-      ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, false);
+  // (holder, block, add?) per stripe, built per part of `changes` (in
+  // parallel for a large batch) and applied stripe by stripe, parts in order
+  using Op = std::tuple<const Address*, const Address*, bool>;
+  const size_t nc = changes.size();
+  const size_t parts = pool && nc >= 2048 ? std::min<size_t>(pool->size() + 1, nc / 1024) : 1;
+  std::vector<std::array<std::vector<Op>, kStripes>> ops(parts);
+  auto build = [&](size_t p) {
+    for (size_t ci = p * nc / parts; ci < (p + 1) * nc / parts; ++ci) {
+      const Change& c = changes[ci];
+      // holders that stayed in place need no membership test (a repair
+      // moves e of k + m)
+      auto same_at = [&](const std::vector<Address>& v, size_t i, const Address& h) {
+        return i < v.size() && v[i] == h;
+      };
+      for (size_t i = 0; i < c.old_h.size(); ++i) {
+        const Address& h = c.old_h[i];
+        if (!h || same_at(c.new_h, i, h) || has(c.new_h, h) ||
+            std::find(c.old_h.begin(), c.old_h.begin() + i, h) != c.old_h.begin() + i)
+          continue;
+        ops[p][AddressHash()(h) % kStripes].emplace_back(&h, &c.block, false);
+      }
+      for (size_t i = 0; i < c.new_h.size(); ++i) {
+        const Address& h = c.new_h[i];
+        if (h && !same_at(c.old_h, i, h) && !has(c.old_h, h))
+          ops[p][AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
+      }
     }
-    for (size_t i = 0; i < c.new_h.size(); ++i) {
-      const Address& h = c.new_h[i];
-      if (h && !same_at(c.old_h, i, h) && !has(c.old_h, h))
-        ops[AddressHash()(h) % kStripes].emplace_back(&h, &c.block, true);
-    }
-  }
+  };
+  if (parts > 1) pool->parallel_for(parts, build);
+  else build(0);
   std::vector<size_t> busy;
   size_t nops = 0;
-  for (size_t si = 0; si < kStripes; ++si)
-    if (!ops[si].empty()) {
-      busy.push_back(si);
-      nops += ops[si].size();
-    }
+  for (size_t si = 0; si < kStripes; ++si) {
+    size_t here = 0;
+    for (auto& op : ops) here += op[si].size();
+    if (here) busy.push_back(si);
+    nops += here;
+  }
   auto apply = [&](size_t t) {
     const size_t si = busy[t];
     Stripe& s = st_[si];
     std::lock_guard<std::mutex> g(s.mu);
-    for (auto& [h, b, add] : ops[si]) {
-      if (add) {
-        s.m[*h].insert(*b);
-      } else {
-        auto it = s.m.find(*h);
-        if (it == s.m.end()) continue;
-        it->second.erase(*b);
-        if (it->second.empty()) s.m.erase(it);
+    for (auto& part : ops)
+      for (auto& [h, b, add] : part[si]) {
+        if (add) {
+          s.m[*h].insert(*b);
+        } else {
+          auto it = s.m.find(*h);
+          if (it == s.m.end()) continue;
+          it->second.erase(*b);
+          if (it->second.empty()) s.m.erase(it);
+        }
       }
-    }
   };
   if (pool && busy.size() > 1 && nops >= 256) pool->parallel_for(busy.size(), apply);
   else
@@ -1628,6 +1639,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       surv_all = arena_.lease(surv_bytes);
       out_all = arena_.lease(out_bytes);
     }
+    tm.lap("alloc");
     const bool pin = rbs.empty() || (surv_all.pinned() && out_all.pinned());
     for (size_t x = 0; x < rbs.size(); ++x) {
       rbs[x].surv = surv_all.data() + o_surv[x];
@@ -1649,10 +1661,14 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         rb.sidx[bi * k + s] = (uint8_t)x.surv[s].first;
       }
       for (int r = 0; r < e; ++r) rb.lidx[bi * e + r] = (uint8_t)x.lost[r];
+    });
+    tm.lap("copy_in");
+    pool_.parallel_for(units.size(), [&](size_t t) {
+      Todo& x = *rbs[units[t].first].grp->items[rbs[units[t].first].b0 + units[t].second];
       x.surv.clear();
       x.surv.shrink_to_fit();
     });
-    tm.lap("copy_in");
+    tm.lap("free");
     if (!rbs.empty()) {
       std::vector<memo_ec_rebuild_segment> segs;
       for (auto& rb : rbs) {
@@ -1673,101 +1689,113 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       ++rep.codec_calls;
       tm.lap("rebuild");
     }
-    for (auto& rb : rbs) {
-      const size_t n = rb.n, S = rb.S;
+    // Place each rebuilt shard on a reachable node holding none of the
+    // block's other shards (Overlay::allocate order); the stale copy on a
+    // reachable old holder is dropped.  One pass over the chunk's blocks,
+    // then one index update for all of them (per batch, the fixed costs of
+    // the two steps outweighed the work at 4 KiB blocks).
+    std::vector<int> placed(units.size(), 0);
+    pool_.parallel_for(units.size(), [&](size_t t) {
+      const RBatch& rb = rbs[units[t].first];
+      const size_t bi = units[t].second, S = rb.S;
       const int e = rb.grp->e;
-      std::vector<int> placed(n, 0);
-      // place each rebuilt shard on a reachable node holding none of the
-      // block's other shards (Overlay::allocate order); the stale copy on
-      // a reachable old holder is dropped
-      pool_.parallel_for(n, [&](size_t bi) {
-        Todo& x = *rb.grp->items[rb.b0 + bi];
-        std::set<Address> taken;
-        for (int i = 0; i < total; ++i)
-          if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
-            taken.insert(x.pl.holder[i]);
-        auto cand = overlay_.allocate(x.a, (int)overlay_.size());
-        const ShardKeys keys(x.a);
-        size_t ci = 0;
-        for (int r = 0; r < e; ++r) {
-          const int i = x.lost[r];
-          const Address old = x.pl.holder[i];
-          const Buffer wire = encode_shard(header_of(x.a, x.pl, i), rb.out + (bi * e + r) * S);
-          x.pl.holder[i] = Address();
-          while (ci < cand.size()) {
-            auto& nd = cand[ci++];
-            if (taken.count(nd->id)) continue;
+      Todo& x = *rb.grp->items[rb.b0 + bi];
+      std::set<Address> taken;
+      for (int i = 0; i < total; ++i)
+        if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
+          taken.insert(x.pl.holder[i]);
+      auto cand = overlay_.allocate(x.a, (int)overlay_.size());
+      const ShardKeys keys(x.a);
+      size_t ci = 0;
+      for (int r = 0; r < e; ++r) {
+        const int i = x.lost[r];
+        const Address old = x.pl.holder[i];
+        const Buffer wire = encode_shard(header_of(x.a, x.pl, i), rb.out + (bi * e + r) * S);
+        x.pl.holder[i] = Address();
+        while (ci < cand.size()) {
+          auto& nd = cand[ci++];
+          if (taken.count(nd->id)) continue;
+          try {
+            nd->store(keys(i), wire);
+            x.pl.holder[i] = nd->id;
+            taken.insert(nd->id);
+            ++placed[t];
+            break;
+          } catch (Unavailable&) {
+          }
+        }
+        if (old && old != x.pl.holder[i]) {
+          auto on = overlay_.node(old);
+          if (on && on->up && !on->evicted) {
             try {
-              nd->store(keys(i), wire);
-              x.pl.holder[i] = nd->id;
-              taken.insert(nd->id);
-              ++placed[bi];
-              break;
-            } catch (Unavailable&) {
+              on->remove(keys(i));
+            } catch (Error&) {
             }
           }
-          if (old && old != x.pl.holder[i]) {
-            auto on = overlay_.node(old);
-            if (on && on->up && !on->evicted) {
+        }
+      }
+    });
+    tm.lap("place");
+    // the chunk's new placements enter the index under one lock
+    // (the changes are built beforehand, on the pool: under the lock only
+    // the lookups and swaps)
+    std::vector<char> gone(units.size(), 0);
+    std::vector<NodeIndex::Change> ch(units.size());
+    pool_.parallel_for(units.size(), [&](size_t t) {
+      const RBatch& rb = rbs[units[t].first];
+      const Todo& x = *rb.grp->items[rb.b0 + units[t].second];
+      ch[t].block = x.a;
+      ch[t].new_h = x.pl.holder;
+    });
+    {
+      std::unique_lock<std::shared_mutex> lk(index_mu_);
+      for (size_t t = 0; t < units.size(); ++t) {
+        const RBatch& rb = rbs[units[t].first];
+        Todo& x = *rb.grp->items[rb.b0 + units[t].second];
+        auto it = index_.find(x.a);
+        if (it == index_.end()) {
+          gone[t] = 1;
+          continue;
+        }
+        ch[t].old_h = std::move(it->second.holder);
+        it->second = std::move(x.pl);  // x.pl unused from here
+      }
+    }
+    tm.lap("swap");
+    for (size_t t = 0; t < units.size(); ++t)
+      if (gone[t]) ch[t].new_h.clear();  // no index change for a removed block
+    nodes_.update_many(ch, &pool_);
+    tm.lap("index");
+    for (size_t t = 0; t < units.size(); ++t) {
+      const RBatch& rb = rbs[units[t].first];
+      const int e = rb.grp->e;
+      Todo& x = *rb.grp->items[rb.b0 + units[t].second];
+      if (gone[t]) {  // removed while being repaired: drop the new shards
+        for (int i : x.lost)
+          if (x.pl.holder[i])
+            if (auto nd = overlay_.node(x.pl.holder[i])) {
               try {
-                on->remove(keys(i));
+                nd->remove(shard_key(x.a, i));
               } catch (Error&) {
               }
             }
-          }
-        }
-      });
-      tm.lap("place");
-      // the batch's new placements enter the index under one lock
-      std::vector<char> gone(n, 0);
-      std::vector<NodeIndex::Change> ch;
-      ch.reserve(n);
-      {
-        std::unique_lock<std::shared_mutex> lk(index_mu_);
-        for (size_t bi = 0; bi < n; ++bi) {
-          Todo& x = *rb.grp->items[rb.b0 + bi];
-          if (!index_.count(x.a)) {
-            gone[bi] = 1;
-            continue;
-          }
-          NodeIndex::Change c;
-          c.block = x.a;
-          c.new_h = x.pl.holder;
-          c.old_h = swap_placement_locked(x.a, std::move(x.pl));  // x.pl unused from here
-          ch.push_back(std::move(c));
-        }
+        continue;
       }
-      nodes_.update_many(ch, &pool_);
-      tm.lap("index");
-      for (size_t bi = 0; bi < n; ++bi) {
-        Todo& x = *rb.grp->items[rb.b0 + bi];
-        if (gone[bi]) {  // removed while being repaired: drop the new shards
-          for (int i : x.lost)
-            if (x.pl.holder[i])
-              if (auto nd = overlay_.node(x.pl.holder[i])) {
-                try {
-                  nd->remove(shard_key(x.a, i));
-                } catch (Error&) {
-                }
-              }
-          continue;
+      ++rep.blocks_repaired;
+      rep.shards_rebuilt += (size_t)placed[t];
+      rep.shards_unplaced += (size_t)e - (size_t)placed[t];
+      ++repaired_;
+      if (rebalanced_ && placed[t]) rebalanced_(x.a);  // moved onto new owners
+      if (placed[t] < e && under_placed_) {
+        // no reachable node could take the rest (Paxos.cc:1120-1126)
+        int held = 0;
+        {
+          std::shared_lock<std::shared_mutex> lk(index_mu_);
+          auto it = index_.find(x.a);
+          if (it != index_.end())
+            for (auto& h : it->second.holder) held += h ? 1 : 0;
         }
-        ++rep.blocks_repaired;
-        rep.shards_rebuilt += (size_t)placed[bi];
-        rep.shards_unplaced += (size_t)e - (size_t)placed[bi];
-        ++repaired_;
-        if (rebalanced_ && placed[bi]) rebalanced_(x.a);  // moved onto new owners
-        if (placed[bi] < e && under_placed_) {
-          // no reachable node could take the rest (Paxos.cc:1120-1126)
-          int held = 0;
-          {
-            std::shared_lock<std::shared_mutex> lk(index_mu_);
-            auto it = index_.find(x.a);
-            if (it != index_.end())
-              for (auto& h : it->second.holder) held += h ? 1 : 0;
-          }
-          under_placed_(x.a, held);
-        }
+        under_placed_(x.a, held);
       }
     }
   }
