@@ -936,11 +936,15 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
     if (b.is_mutable || b.address.mutable_block()) backend_->store(b, STORE_INSERT);
     else imm.push_back(&b);
   }
-  // The per-block host work (CHB address check, copies into the batch,
-  // shard framing + stores) runs on the pool, one block per task; the
-  // encode is one GPU call per shard-size bucket.
-  for (size_t b0 = 0; b0 < imm.size(); b0 += o_.batch_max) {
-    const size_t n0 = std::min<size_t>(o_.batch_max, imm.size() - b0);
+  // Chunks of up to stage_bytes of shards: the per-block host work (CHB
+  // address check, copies into the batch, shard framing + stores) runs on
+  // the pool over a whole chunk, and the encode is one GPU call per
+  // shard-size bucket of it (thousands of 4 KiB blocks per pass: the pool's
+  // fixed costs per pass stay small beside the work).
+  for (size_t b0 = 0, n0 = 0; b0 < imm.size(); b0 += n0) {
+    size_t bytes = 0;
+    for (n0 = 0; b0 + n0 < imm.size() && (n0 == 0 || bytes < o_.stage_bytes); ++n0)
+      bytes += (size_t)(o_.k + o_.m) * memo_ec_shard_size(imm[b0 + n0]->data.size(), o_.k);
     PhaseTimer tm("store_many");
     std::vector<char> valid(n0, 0);
     pool_.parallel_for(n0, [&](size_t i) {

@@ -144,8 +144,8 @@ class PinnedArena {
   size_t keep_;
 };
 
-// Default survivor bytes one fetch or repair stages (pinned) and hands to
-// one codec call at most (ErasureOptions::stage_bytes).
+// Default shard bytes one store_many, fetch or repair chunk stages (pinned)
+// and hands to one codec call at most (ErasureOptions::stage_bytes).
 constexpr size_t kStageBytes = (size_t)512 << 20;
 
 // ---------------------------------------------------------- shard format
@@ -253,7 +253,7 @@ class NodeIndex {
 struct ErasureOptions {
   int k = 10, m = 4;
   int device = -1;             // < 0: every GPU the library sees
-  int batch_max = 256;         // blocks per GPU encode / rebuild call
+  int batch_max = 256;         // blocks per batcher encode call / rebuild batch
   int batch_window_us = 200;   // how long the batcher waits for company
   int threads = 16;            // peer fan-out (memo's background pool is <= 16)
   // Blocks of one batch that share an erasure pattern (the repair of one
@@ -263,8 +263,8 @@ struct ErasureOptions {
   // the rest to the per-block rebuild.
   int uniform_min = 4;
   size_t uniform_min_bytes = 8u << 20;
-  // Survivor bytes a fetch or repair stages (pinned) per codec call at most;
-  // larger requests run as several such chunks.
+  // Shard bytes a store_many (data + parity), fetch or repair (survivors)
+  // stages (pinned) per chunk at most; larger requests run as several chunks.
   size_t stage_bytes = kStageBytes;
   // A node that disappears is evicted -- its shards rebuilt elsewhere --
   // after this long unless it comes back ("eviction-delay", Paxos.cc:985-1009,
