@@ -410,8 +410,8 @@ def test_bench_default_line_runs_every_leg():
     """The driver's own command shape at N = 1 (fewer steps, a short CPU
     sample): the line carries the whole-batch oracle comparison of C2, C3,
     the 4 KiB rebuilds and C5, the achievable-rate probe, the 4 KiB counter
-    summary, counter traffic, the CPU baseline, the device identity and the
-    plugin-level lines."""
+    summary, counter traffic, the CPU baseline, the device identity, the
+    SHA-256 lines and the plugin-level lines."""
     import subprocess
     import sys
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "5",
@@ -430,6 +430,8 @@ def test_bench_default_line_runs_every_leg():
     assert res["roofline"]["traffic_ratio"] < 1.1
     assert res["cpu_baseline"]["bit_exact_vs_gpu"] and res["c1"]["bit_exact"]
     assert res["ranks"]["per_gpu"][0]["uuid"] and res["build_matches_sources"]
+    for key in ("C2 batch, 1 MiB blocks", "4 KiB blocks"):
+        assert res["sha256"][key]["bit_exact"] and res["sha256"][key]["checked"] >= 4096, res["sha256"]
     for key, pl in res["plugin"].items():
         assert pl["ok"] and pl["erasure"]["fetch_after_repair_ok"], (key, pl)
         assert pl["erasure"]["unrecoverable"] == 0 and pl["erasure"]["degraded_codec_calls"] >= 1
@@ -453,3 +455,17 @@ def test_plugin_lines_parse_and_flag_failures(tmp_path):
     assert not out["5x64"]["ok"]
     gone = bench.plugin_lines(str(tmp_path / "missing"), [(1, 1)], timeout=30)
     assert not gone["1x1"]["ok"] and gone["1x1"]["note"]
+
+
+def test_sha_digest_check_catches_one_flipped_byte():
+    """bench.py's hashlib check of GPU digests (no GPU: digests made here)."""
+    import hashlib
+    import bench
+    rng = np.random.default_rng(SEED)
+    msgs = rng.integers(0, 256, size=(40, 300), dtype=np.uint8)
+    digs = np.stack([np.frombuffer(hashlib.sha256(bytes(64) + m[:257].tobytes()).digest(), np.uint8)
+                     for m in msgs])
+    assert bench.sha_digests_ok(msgs, digs, range(40), 257, 4)
+    digs[17, 3] ^= 1
+    assert not bench.sha_digests_ok(msgs, digs, range(40), 257, 4)
+    assert bench.sha_digests_ok(msgs, digs, range(17), 257, 1)
