@@ -1,6 +1,6 @@
 """Fused mixed-geometry encode (memo_ec_encode_segments) against the same
 segments launched one by one, for one library build.  Run on the GPU box:
-  python tools/fused_probe.py [--lib memo_amd/_lib/variants/lib_noxcd.so]
+  python tools/fused_probe.py [--lib <another libmemo_ec.so build>]
 One JSON line.
 """
 import argparse

@@ -47,9 +47,7 @@ def main():
         c.encode(k, m, d, p)
         c.rebuild(k, m, sd, surv, ld, out)
         torch.cuda.synchronize()
-    res = {"k": k, "m": m, "B": B, "n": n, "e": e, "S": S, "path": c.rebuild_path(n, k, S),
-           "decode_chunks": os.environ.get("MEMO_EC_DECODE_CHUNKS", "default"),
-           "decode_table": os.environ.get("MEMO_EC_DECODE_TABLE", "default")}
+    res = {"k": k, "m": m, "B": B, "n": n, "e": e, "S": S, "path": c.rebuild_path(n, k, S)}
     for name, fn, alg in (("encode", lambda: c.encode(k, m, d, p), (k + m) * S * n),
                           ("rebuild", lambda: c.rebuild(k, m, sd, surv, ld, out), (k + e) * S * n)):
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
