@@ -800,7 +800,7 @@ def pmc_traffic(args, result, local, world):
         env[var] = dev
     child = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--steps", "3", "--warmup", "1",
              "--settle-ms", "0", "--no-small", "--no-cpu", "--no-e2e", "--no-pmc", "--no-verify",
-             "--no-c5",
+             "--no-c5", "--no-plugin", "--no-sha",
              "--k", str(k), "--m", str(m), "--block-bytes", str(B), "--blocks", str(n),
              "--erasures", str(e)]
 

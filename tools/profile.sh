@@ -6,8 +6,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/prof}
-ARGS=${ARGS:---no-cpu --no-e2e --no-small --no-pmc --no-verify --no-c5}
-PMC_ARGS=${PMC_ARGS:---no-cpu --no-e2e --no-small --no-pmc --no-verify --no-c5 --steps 4 --warmup 2 --settle-ms 0}
+ARGS=${ARGS:---no-cpu --no-e2e --no-small --no-pmc --no-verify --no-c5 --no-plugin --no-sha}
+PMC_ARGS=${PMC_ARGS:---no-cpu --no-e2e --no-small --no-pmc --no-verify --no-c5 --no-plugin --no-sha --steps 4 --warmup 2 --settle-ms 0}
 mkdir -p $OUT
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/trace -o trace -f csv -- python3 bench.py $ARGS > $OUT/trace.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch -f csv -- python3 bench.py $PMC_ARGS > $OUT/fetch.log 2>&1 || exit $?
