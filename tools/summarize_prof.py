@@ -73,7 +73,8 @@ def main():
                 f.write("%s,%d,%.1f,%.1f\n" % (kd, i, a, b))
     md = ["# %s profile: RS(10,4) encode (C2) + 4-erasure rebuild (C3), 4096 x 1 MiB blocks, 1 MI355X" % tag,
           "", "Command: `tools/profile.sh` -- rocprofv3 --kernel-trace --stats on `python3 bench.py "
-          "--no-cpu --no-e2e --no-small` (the contract's step: one encode + one rebuild); then "
+          "--no-cpu --no-e2e --no-small --no-pmc --no-verify --no-c5 --no-plugin --no-sha` (the "
+          "contract's step: one encode + one rebuild, and the achievable-rate probe); then "
           "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes, each its own run.", "",
           "| kernel | calls | avg us | min us | max us |", "|---|---|---|---|---|"]
     for r in rows(stats):
