@@ -468,6 +468,42 @@ TEST(remove_with_holder_down, true) {
   CHECK(net.shards(c.address, 14) == 14);
 }
 
+// store_many stages at most stage_bytes of shards per chunk: several encode
+// calls for a request larger than that, mixed block sizes within a chunk,
+// every shard on its owner and every block reads back; a block whose owners
+// are too few does not stop the others.
+TEST(store_many_stages_in_chunks, true) {
+  Net net(16, 10, 4);
+  net.o.stage_bytes = 1u << 20;  // ~7 blocks of 100 KiB (14 x 10 KiB shards each)
+  net.restart();
+  std::vector<Block> blocks;
+  for (int i = 0; i < 40; ++i)
+    blocks.push_back(make_chb(random_bytes(i % 5 == 0 ? 3000 : 100000 + 37 * i, 4000 + i)));
+  const uint64_t calls0 = net.ec->codec().encode_calls();
+  net.ec->store_many(blocks);
+  CHECK(net.ec->codec().encode_calls() - calls0 >= 5);
+  for (auto& b : blocks) {
+    CHECK(net.holders(b.address, 14) == 14);
+    CHECK(net.ec->fetch(b.address)->data == b.data);
+  }
+  // 6 of 16 nodes down: 10 reachable owners, every block still stored
+  for (int i = 0; i < 6; ++i) net.nodes[i]->up = false;
+  std::vector<Block> more;
+  for (int i = 0; i < 12; ++i) more.push_back(make_chb(random_bytes(50000, 5000 + i)));
+  net.ec->store_many(more);
+  for (auto& b : more) CHECK(net.ec->fetch(b.address)->data == b.data);
+  // 7 down: 9 reachable owners, below k -- TooFewPeers
+  net.nodes[6]->up = false;
+  std::vector<Block> last{make_chb(random_bytes(50000, 6000))};
+  bool threw = false;
+  try {
+    net.ec->store_many(last);
+  } catch (TooFewPeers&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
 // A large degraded multi-fetch (a node-loss event) stages its survivors in
 // chunks of at most stage_bytes: one lease pair and one codec call per
 // chunk, every block right, and no outsized pinned buffer kept afterwards.
