@@ -2045,8 +2045,9 @@ void ErasureConsensus::membership_loop() {
 }
 
 // "erasure" configuration: {"type": "erasure", "data-shards": k,
-// "parity-shards": m, "backend-replication-factor": f}; kebab-case keys as
-// "replication-factor" (Paxos.cc:2273-2276).
+// "parity-shards": m, "backend-replication-factor": f, and optionally
+// "device", "batch-max", "eviction-delay" (s), "stage-mb", "threads"};
+// kebab-case keys as "replication-factor" (Paxos.cc:2273-2276).
 namespace {
 struct RegisterErasure {
   RegisterErasure() {
@@ -2061,6 +2062,10 @@ struct RegisterErasure {
       o.device = get("device", 0);
       o.batch_max = get("batch-max", 256);
       o.eviction_delay_ms = (int64_t)get("eviction-delay", 600) * 1000;  // seconds
+      o.stage_bytes = (size_t)get("stage-mb", (int)(kStageBytes >> 20)) << 20;
+      o.threads = get("threads", o.threads);
+      if (o.batch_max < 1 || o.stage_bytes == 0 || o.threads < 1)
+        throw Error("erasure: batch-max, stage-mb and threads must be positive");
       const int f = get("backend-replication-factor", 3);
       return std::unique_ptr<Consensus>(
           new ErasureConsensus(std::make_unique<ReplicationConsensus>(ov, f), ov, o));
