@@ -728,7 +728,7 @@ def sha_digests_ok(msgs, digs, idx, bb, threads):
     def one(i):
         return hashlib.sha256(pre + msgs[i, :bb].tobytes()).digest() == digs[i].tobytes()
     with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
-        return all(ex.map(one, idx, chunksize=256))
+        return all(ex.map(one, idx))
 
 
 def sha_lines(torch, codec, stream, data, n, B, threads=1):
