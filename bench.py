@@ -94,7 +94,10 @@ def parse(argv=None):
 def log(msg):
     """Progress on stderr (stdout carries only the JSON line): long runs keep
     showing signs of life."""
-    print("[bench %.1fs] %s" % (time.perf_counter() - _T0, msg), file=sys.stderr, flush=True)
+    # one write per line: ranks share the stream, and print() writes the
+    # text and the newline separately
+    sys.stderr.write("[bench %.1fs] %s\n" % (time.perf_counter() - _T0, msg))
+    sys.stderr.flush()
 
 
 _T0 = time.perf_counter()
