@@ -3,6 +3,7 @@ the golden fixtures, bit-exact.  Full-size configs (BASELINE.json C2/C3)
 are checked through size-independent properties (rebuild round trips,
 sampled blocks against the oracle)."""
 import itertools
+import os
 
 import numpy as np
 import pytest
@@ -90,12 +91,13 @@ def test_encode_rebuild_vs_oracle(codec, O, k, m, rebuild_path):
             assert np.array_equal(host(out), O.gather(k, m, S, data, want, l)), (k, m, B, e)
 
 
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MEMO_EC_STRESS_SEEDS", "6"))))
 def test_random_geometries_vs_oracle(codec, O, seed, rebuild_path):
     """Seeded random codes and sizes (k 1..24, m 1..10, B 1..200000 B, 1..12
     blocks, any e <= m, every block its own erasure pattern in a random
     survivor order), device and pageable-host buffers, encode, per-block
-    rebuild and the one-pattern rebuild, all against the oracle."""
+    rebuild and the one-pattern rebuild, all against the oracle.
+    MEMO_EC_STRESS_SEEDS widens the seed range for a longer run."""
     rng = np.random.default_rng(0xC0DE + seed)
     for it in range(4):
         k, m = int(rng.integers(1, 25)), int(rng.integers(1, 11))
