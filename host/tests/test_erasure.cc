@@ -470,6 +470,112 @@ TEST(remove_with_holder_down, true) {
   CHECK(net.shards(c.address, 14) == 14);
 }
 
+// Seeded random operations and membership changes: batched and single
+// stores of mixed sizes, nodes going down and coming back (overlay events,
+// so the membership thread runs its expansions and settles removals
+// concurrently), evictions with their repair, removals.  After every step:
+// with at most m nodes unreachable every live block reads back (multi-fetch
+// and single fetch) bit-exact; a removed block does not; after an eviction
+// every live block again has k + m shards on nodes that are not evicted.
+// MEMO_EC_CHAOS_RUNS=N runs N seeds (default 1).
+static void chaos_run(uint64_t run_seed) {
+  const int k = 10, m = 4, total = k + m;
+  Net net(22, k, m);  // at most 4 evictions leave 18 >= k + m nodes
+  std::mt19937_64 rng(0x5EED0001 + run_seed);
+  std::vector<std::pair<Address, Buffer>> live;
+  std::vector<Address> removed;
+  int evictions = 0;
+  uint64_t seed = 7000 + run_seed * 1000;
+  auto pick = [&](auto pred) -> std::shared_ptr<Node> {
+    std::vector<std::shared_ptr<Node>> c;
+    for (auto& n : net.nodes)
+      if (pred(*n)) c.push_back(n);
+    return c.empty() ? nullptr : c[rng() % c.size()];
+  };
+  auto down_count = [&] {
+    int d = 0;
+    for (auto& n : net.nodes) d += !n->up && !n->evicted;
+    return d;
+  };
+  auto random_size = [&]() -> size_t {
+    switch (rng() % 4) {
+      case 0: return 4096;
+      case 1: return 1 + rng() % 2000;
+      case 2: return 1 + rng() % 200000;
+      default: return 1 << 20;
+    }
+  };
+  for (int step = 0; step < 60; ++step) {
+    const int op = (int)(rng() % 7);
+    if (op == 0 || op == 1) {  // a batch, or one block
+      std::vector<Block> bs;
+      const int nb = op == 0 ? 1 + (int)(rng() % 40) : 1;
+      for (int i = 0; i < nb; ++i) bs.push_back(make_chb(random_bytes(random_size(), ++seed)));
+      if (op == 0) net.ec->store_many(bs);
+      else net.ec->store(bs[0]);
+      for (auto& b : bs) live.emplace_back(b.address, b.data);
+    } else if (op == 2) {  // a node goes down
+      if (down_count() < m)
+        if (auto n = pick([](const Node& x) { return x.up && !x.evicted; })) net.overlay.set_up(n->id, false);
+    } else if (op == 3) {  // a node comes back
+      if (auto n = pick([](const Node& x) { return !x.up && !x.evicted; })) net.overlay.set_up(n->id, true);
+    } else if (op == 4) {  // a down node is evicted: its shards rebuilt elsewhere
+      if (evictions < 4)
+        if (auto n = pick([](const Node& x) { return !x.up && !x.evicted; })) {
+          const auto rep = net.ec->evict(n->id);
+          ++evictions;
+          CHECK(rep.unrecoverable == 0);
+          for (auto& [a, d] : live) CHECK(net.shards(a, total) >= total);
+        }
+    } else if (op == 5 && !live.empty()) {  // a removal
+      const size_t x = rng() % live.size();
+      net.ec->remove(live[x].first);
+      removed.push_back(live[x].first);
+      live.erase(live.begin() + (long)x);
+    } else if (op == 6 && !live.empty()) {  // one block alone
+      const auto& [a, d] = live[rng() % live.size()];
+      CHECK(net.ec->fetch(a)->data == d);
+    }
+    // every live block, in one multi-fetch
+    std::vector<Address> req;
+    for (auto& [a, d] : live) req.push_back(a);
+    size_t ok = 0;
+    net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
+      for (auto& [x, d] : live)
+        if (x == a && b && b->data == d) ++ok;
+    });
+    CHECK(ok == live.size());
+    if (ok != live.size()) {
+      std::fprintf(stderr, "  seed %llu step %d op %d: %zu of %zu live blocks read back\n",
+                   (unsigned long long)run_seed, step, op, ok, live.size());
+      return;
+    }
+    for (auto& a : removed) {
+      bool gone = false;
+      try {
+        net.ec->fetch(a);
+      } catch (MissingBlock&) {
+        gone = true;
+      } catch (TooFewPeers&) {
+        gone = true;  // holders of its last shards down: "out of reach"
+      }
+      CHECK(gone);
+    }
+  }
+  std::printf("  (seed %llu: %zu live, %zu removed, %d evictions)\n", (unsigned long long)run_seed,
+              live.size(), removed.size(), evictions);
+}
+
+TEST(randomized_membership_and_operations, true) {
+  const char* e = std::getenv("MEMO_EC_CHAOS_RUNS");
+  const int runs = e ? std::max(1, std::atoi(e)) : 1;
+  for (int r = 0; r < runs; ++r) {
+    const int before = g_fail;
+    chaos_run((uint64_t)r);
+    if (g_fail != before) break;
+  }
+}
+
 // store_many stages at most stage_bytes of shards per chunk: several encode
 // calls for a request larger than that, mixed block sizes within a chunk,
 // every shard on its owner and every block reads back; a block whose owners
