@@ -4,6 +4,8 @@ per-block or shared erasure patterns -- the read side of the reference's
 multi-address fetch, which hands a whole batch over at once
 (src/memo/model/doughnut/Consensus.cc:101-124, consensus/Paxos.cc:1857-1890).
 Every rebuilt shard is compared with the CPU oracle's shards, bit-exact."""
+import os
+
 import numpy as np
 import pytest
 
@@ -191,3 +193,34 @@ def test_mixed_codes_any_k(codec, O, spec, rebuild_path):
     codec.synchronize()
     for g, s in zip(groups, segs):
         assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (g["k"], g["m"], g["S"], g["e"])
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("MEMO_EC_STRESS_SEEDS", "4"))))
+def test_random_segments_vs_oracle(codec, O, seed, rebuild_path):
+    """Seeded random mixed calls: 1..12 segments of random (k 1..24, m 1..10,
+    B 1..300000 B, n 1..8, e 1..m, per-block or shared pattern), one
+    encode_segments call and one rebuild_segments call, device-resident,
+    every parity and rebuilt byte against the oracle.  MEMO_EC_STRESS_SEEDS
+    widens the seed range for a longer run."""
+    rng = np.random.default_rng(0x5E6 + seed)
+    spec = []
+    for _ in range(int(rng.integers(1, 13))):  # MEMO_EC_MAX_SEGMENTS
+        k, m = int(rng.integers(1, 25)), int(rng.integers(1, 11))
+        spec.append((k, m, int(rng.integers(1, 300001)), int(rng.integers(1, 9)), int(rng.integers(1, m + 1)),
+                     bool(rng.integers(0, 2))))
+    # encode: the data of every segment in one call
+    enc = []
+    for gi, (k, m, B, n, e, uni) in enumerate(spec):
+        S = O.shard_size(B, k)
+        data = O.fill_blocks(SEED, 7919 * gi + seed, n, B, k, S)
+        enc.append((k, m, S, n, dev(data), empty(n, m * S), O.encode(k, m, S, data, threads=4)))
+    codec.encode_segments([x[:6] for x in enc])
+    codec.synchronize()
+    for gi, x in enumerate(enc):
+        assert np.array_equal(x[5].cpu().numpy(), x[6]), (seed, gi, spec[gi])
+    groups = make_groups(O, spec, seed)
+    segs = device_segs(groups)
+    codec.rebuild_segments(segs)
+    codec.synchronize()
+    for gi, (g, s) in enumerate(zip(groups, segs)):
+        assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (seed, gi, spec[gi])
