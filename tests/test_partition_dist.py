@@ -426,7 +426,7 @@ def test_bench_default_line_runs_every_leg():
         assert 0 < sm["frac_of_achievable"] <= 1.05
         assert set(sm["counters"]) == {"encode MAC", "rebuild MAC", "decode rows"}, res["rebuild_small"]
     assert res["c5_mixed"]["oracle_bit_exact"] and len(res["c5_mixed"]["groups"]) == 12
-    assert 0 < res["roofline"]["frac_of_achievable"] <= 1.0
+    assert 0 < res["roofline"]["frac_of_achievable"] <= 1.05  # probe timing noise: a few %
     assert res["roofline"]["traffic_ratio"] < 1.1
     assert res["cpu_baseline"]["bit_exact_vs_gpu"] and res["c1"]["bit_exact"]
     assert res["ranks"]["per_gpu"][0]["uuid"] and res["build_matches_sources"]
