@@ -185,7 +185,7 @@ def sweep(torch, ec, codec, stream, gib, steps, warmup, settle_ms, cpu=True):
             pt = {"k": k, "m": m, "block_bytes": B, "blocks": n, "shard_bytes": S,
                   "kernel_ms": round(ms, 4), "GiBs": round(n * B / (ms * 1e-3) / 2**30, 1),
                   "frac": frac((k + m) * S * n, ms),
-                  "rebuild": {"erasures": e, "kernel": codec.rebuild_path(n, k, S), "step_ms": round(rs, 4),
+                  "rebuild": {"erasures": e, "kernel": codec.rebuild_path(n, k, S, e), "step_ms": round(rs, 4),
                               "GiBs": round(n * B / (rs * 1e-3) / 2**30, 1),
                               "frac": frac((k + e) * S * n, rs),
                               "bit_exact": bool(torch.equal(out, want))},
@@ -1258,7 +1258,7 @@ def main():
         extra["oracle"] = {"C2_encode": verify_encode(stage, k, m, S, data, par, vthreads)}
         if e > 0:
             vr = verify_rebuild(stage, k, m, S, s_idx, surv, l_idx, out, vthreads)
-            vr["path"] = codec.rebuild_path(n, k, S)
+            vr["path"] = codec.rebuild_path(n, k, S, e)
             extra["oracle"]["C3_rebuild"] = vr
         del stage
     if e > 0:

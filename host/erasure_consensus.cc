@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <optional>
+#include <random>
 #include <set>
 #include <unordered_map>
 
@@ -507,6 +508,10 @@ ErasureConsensus::ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& 
       pool_(o.threads) {
   if (o_.k < 1 || o_.m < 1 || o_.k > MEMO_EC_MAX_K || o_.m > MEMO_EC_MAX_M)
     throw Error("erasure: bad (k, m)");
+  if (o_.fetch_hedge < 0 || o_.verify_subsets < 0) throw Error("erasure: bad fetch-hedge / verify-subsets");
+  // elle::os::getenv("INFINIT_DISABLE_BALANCED_TRANSFERS", false) (Paxos.cc:488-489)
+  if (const char* v = std::getenv("INFINIT_DISABLE_BALANCED_TRANSFERS"))
+    if (*v && std::string(v) != "0" && std::string(v) != "false") o_.balanced_transfers = false;
   // the index first: rescan() may throw (silo listing), and must do so before
   // any thread of this object exists
   if (o_.rescan) rescan();
@@ -577,6 +582,8 @@ std::string ErasureConsensus::stats() const {
                   {"decoded", std::to_string(decoded_)},
                   {"repaired", std::to_string(repaired_)},
                   {"evictions", std::to_string(evictions_)},
+                  {"subset_recoveries", std::to_string(subset_recoveries_)},
+                  {"corrupt_shards_rewritten", std::to_string(corrupt_rewritten_)},
                   {"pending_evictions", std::to_string(pending_evictions())},
                   {"encode_calls", std::to_string(codec_.encode_calls())},
                   {"rebuild_calls", std::to_string(codec_.rebuild_calls())}});
@@ -853,7 +860,9 @@ std::exception_ptr ErasureConsensus::place_batch(const std::vector<const Block*>
       try {
         nd->store((*keys[i])(j), encode_shard(hdr[i], p, j));
         ok[e] = 1;
-      } catch (Unavailable&) {
+      } catch (Error&) {
+        // unreachable (Unavailable) or refused (silo::InsufficientSpace, ...):
+        // a shard not placed, so the placement below records what did land
       }
     }
   });
@@ -997,7 +1006,8 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
 std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
                                                                     bool& any_down,
                                                                     ShardHeader* hdr,
-                                                                    bool parallel) {
+                                                                    bool parallel,
+                                                                    std::vector<Node*>* from) {
   const int total = o_.k + o_.m;
   // the shard keys (one SHA-256 for the block), outside the parallel fetches
   std::vector<Key> keys(total);
@@ -1022,6 +1032,13 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   auto try_node = [&](const std::shared_ptr<Node>& nd, int i) -> bool {
     Buffer wire;
     try {
+      // in flight from this client (Paxos.cc:506-507), for the ordering below
+      std::atomic<int>& tr = transfers(nd.get());
+      tr.fetch_add(1, std::memory_order_relaxed);
+      struct Done {
+        std::atomic<int>& t;
+        ~Done() { t.fetch_sub(1, std::memory_order_relaxed); }
+      } done{tr};
       if (!nd->try_fetch(keys[i], wire)) return true;
     } catch (Unavailable&) {
       std::lock_guard<std::mutex> g(gm);
@@ -1038,7 +1055,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
       } else if (!h.same_block(ref)) {
         return true;  // another geometry, salt or owner: an erasure
       }
-      got.emplace(i, std::move(wire));
+      if (got.emplace(i, std::move(wire)).second && from) (*from)[i] = nd.get();
     } catch (ValidationFailed&) {
       // corrupted shard: an erasure
     }
@@ -1061,18 +1078,53 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
         if (it->second.holder[i]) holder[i] = overlay_.node(it->second.holder[i]);
     }
   }
-  for (int pass = 0; pass < 2 && count() < want; ++pass) {
-    // pass 0: the data shards (no decode needed); pass 1: the parity shards
+  // the recorded holders of shards [i0, i1) worth asking (known-down ones
+  // are skipped, without a fetch or an exception)
+  auto candidates = [&](int i0, int i1) {
     std::vector<int> ids;
-    for (int i = pass ? o_.k : 0; i < (pass ? total : o_.k); ++i) {
+    for (int i = i0; i < i1; ++i) {
       if (!holder[i] || holder[i]->evicted || have(i)) continue;
-      if (!holder[i]->up) {  // known down: no fetch (and no exception) for it
+      if (!holder[i]->up) {
+        std::lock_guard<std::mutex> g(gm);
         any_down = true;
         continue;
       }
       ids.push_back(i);
     }
+    return ids;
+  };
+  // pass 0: the data shards (no decode needed), all at once
+  {
+    const std::vector<int> ids = candidates(0, std::min(o_.k, total));
     run(ids.size(), [&](size_t t) { try_node(holder[ids[t]], ids[t]); });
+  }
+  // pass 1: only as many parity shards as the decode still needs (+ the
+  // configured hedge on the first round), topped up from the remaining
+  // holders while fetches fail.  The holders are shuffled, then taken in
+  // order of in-flight transfers from this client, as the reference orders
+  // a block's replicas (Paxos.cc:488-500; INFINIT_DISABLE_BALANCED_TRANSFERS
+  // turns it off).
+  if (count() < want) {
+    std::vector<int> ids = candidates(o_.k, total);
+    if (o_.balanced_transfers && ids.size() > 1) {
+      thread_local std::mt19937_64 rng(std::random_device{}());
+      std::shuffle(ids.begin(), ids.end(), rng);
+      std::vector<std::pair<int, int>> load;
+      for (int i : ids) load.push_back({transfers(holder[i].get()).load(std::memory_order_relaxed), i});
+      std::stable_sort(load.begin(), load.end(),
+                       [](const auto& x, const auto& y) { return x.first < y.first; });
+      for (size_t t = 0; t < ids.size(); ++t) ids[t] = load[t].second;
+    }
+    size_t next = 0;
+    int hedge = o_.fetch_hedge;
+    while (next < ids.size()) {
+      const int need = want - count();
+      if (need <= 0) break;
+      const size_t n = std::min(ids.size() - next, (size_t)(need + hedge));
+      hedge = 0;
+      run(n, [&](size_t t) { try_node(holder[ids[next + t]], ids[next + t]); });
+      next += n;
+    }
   }
 
   if (count() < want) {
@@ -1138,7 +1190,7 @@ std::unique_ptr<Block> ErasureConsensus::assemble(const Address& a, Gathered& g,
     std::memcpy(block.data() + (size_t)g.lost[r] * S, rebuilt + r * stride, S);
   block.resize(g.h.block_size);
   if (!chb_valid(a, g.h.salt, g.h.owner, block))
-    throw ValidationFailed("erasure: reassembled block does not match its address");
+    throw AddressMismatch("erasure: reassembled block does not match its address");
   auto b = std::make_unique<Block>();
   b->address = a;
   b->data = std::move(block);
@@ -1168,7 +1220,132 @@ std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
                    out.data());
     ++decoded_;
   }
-  return assemble(a, g, out.data(), g.h.shard_size);
+  try {
+    return assemble(a, g, out.data(), g.h.shard_size);
+  } catch (AddressMismatch&) {
+    if (o_.verify_subsets == 0) throw;
+    return recover(a, true);
+  }
+}
+
+namespace {
+// Next combination c (ascending, |c| = d) of {0..n-1}; false after the last.
+bool next_combination(std::vector<int>& c, int n) {
+  const int d = (int)c.size();
+  for (int i = d - 1; i >= 0; --i)
+    if (c[i] < n - d + i) {
+      ++c[i];
+      for (int j = i + 1; j < d; ++j) c[j] = c[j - 1] + 1;
+      return true;
+    }
+  return false;
+}
+
+// k-subsets of n shards in hand (positions, sorted by shard index: the
+// first k are the lowest indices), in order of how many of the first k they
+// replace by spares -- the first k themselves, then one wrong shard is
+// found among the next k * (n - k) -- at most `limit` of them.  (The first
+// k may differ from the failed attempt's: that one decoded from whichever
+// parity holders answered first.)
+std::vector<std::vector<int>> retry_subsets(int n, int k, int limit) {
+  std::vector<std::vector<int>> out;
+  const int spare = n - k;
+  for (int d = 0; d <= std::min(spare, k); ++d) {
+    std::vector<int> drop(d);
+    for (int i = 0; i < d; ++i) drop[i] = i;
+    do {
+      std::vector<int> add(d);
+      for (int i = 0; i < d; ++i) add[i] = i;
+      do {
+        if ((int)out.size() >= limit) return out;
+        std::vector<int> sub;
+        for (int p = 0, q = 0; p < k; ++p) {
+          if (q < d && drop[q] == p) {
+            ++q;
+            continue;
+          }
+          sub.push_back(p);
+        }
+        for (int x : add) sub.push_back(k + x);
+        out.push_back(std::move(sub));
+      } while (next_combination(add, spare));
+    } while (next_combination(drop, k));
+  }
+  return out;
+}
+}  // namespace
+
+// The reassembly of `a` failed its CHB address although every shard passed
+// its CRC: a holder returned a well-framed shard with the wrong bytes.  The
+// reference moves on to the next replica on any error (Paxos.cc:502-517);
+// with erasure coding the other shards can out-vote the wrong one.  Every
+// reachable shard is fetched, k-subsets are decoded until one reassembles to
+// the address (at most verify_subsets), and each shard in hand that
+// disagrees with the verified block is rewritten on its holder.
+std::unique_ptr<Block> ErasureConsensus::recover(const Address& a, bool parallel) {
+  const int k = o_.k, m = o_.m, total = k + m;
+  const std::string what = "erasure: reassembled block does not match its address";
+  bool any_down = false;
+  ShardHeader h;
+  std::vector<Node*> from(total, nullptr);
+  auto have = gather_shards(a, total, any_down, &h, parallel, &from);
+  std::sort(have.begin(), have.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  const int n = (int)have.size();
+  if (n <= k) throw AddressMismatch(what + " (no spare shard to try)");
+  const size_t S = h.shard_size;
+  std::vector<uint8_t> sidx(k), lost;
+  Buffer surv((size_t)k * S), out((size_t)m * S), block;
+  for (const auto& sub : retry_subsets(n, k, o_.verify_subsets)) {
+    std::vector<bool> present(k, false);
+    block.assign((size_t)k * S, 0);
+    for (int t = 0; t < k; ++t) {
+      const auto& sh = have[sub[t]];
+      sidx[t] = (uint8_t)sh.first;
+      const uint8_t* pay = sh.second.data() + ShardHeader::kSize;
+      std::memcpy(surv.data() + (size_t)t * S, pay, S);
+      if (sh.first < k) {
+        present[sh.first] = true;
+        std::memcpy(block.data() + (size_t)sh.first * S, pay, S);
+      }
+    }
+    lost.clear();
+    for (int j = 0; j < k; ++j)
+      if (!present[j]) lost.push_back((uint8_t)j);
+    if (!lost.empty()) {
+      codec_.rebuild(k, m, S, 1, sidx.data(), surv.data(), lost.data(), (int)lost.size(), out.data());
+      for (size_t r = 0; r < lost.size(); ++r)
+        std::memcpy(block.data() + (size_t)lost[r] * S, out.data() + r * S, S);
+    }
+    Buffer padded_block = block;  // k x S, the verified shards
+    block.resize(h.block_size);
+    if (!chb_valid(a, h.salt, h.owner, block)) continue;
+    // the block is verified: every shard in hand that differs from its
+    // re-encoding is rewritten on the holder that served it
+    Buffer parity((size_t)m * S);
+    codec_.encode(k, m, S, 1, padded_block.data(), parity.data());
+    const ShardKeys keys(a);
+    for (const auto& sh : have) {
+      const int i = sh.first;
+      const uint8_t* want = i < k ? padded_block.data() + (size_t)i * S : parity.data() + (size_t)(i - k) * S;
+      if (std::memcmp(sh.second.data() + ShardHeader::kSize, want, S) == 0 || !from[i]) continue;
+      try {
+        from[i]->store(keys(i), encode_shard(h, want, i));
+        ++corrupt_rewritten_;
+      } catch (Error&) {
+        // unreachable now: the next fetch or repair meets it again
+      }
+    }
+    ++subset_recoveries_;
+    ++fetched_;
+    auto b = std::make_unique<Block>();
+    b->address = a;
+    b->data = std::move(block);
+    b->salt = h.salt;
+    b->owner = h.owner;
+    return b;
+  }
+  throw AddressMismatch(what + " (no k-subset of the " + std::to_string(n) +
+                        " reachable shards matches)");
 }
 
 // Multi-address fetch: shards of all blocks gathered on the pool, then ONE
@@ -1235,7 +1412,12 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
   for (auto& r : rest) groups.push_back({(int)r.first.second, false, {}, r.second});
   auto finish = [&](size_t i, const uint8_t* rebuilt, size_t stride) {
     try {
-      blocks[i] = assemble(addresses[i], g[i], rebuilt, stride);
+      try {
+        blocks[i] = assemble(addresses[i], g[i], rebuilt, stride);
+      } catch (AddressMismatch&) {
+        if (o_.verify_subsets == 0) throw;
+        blocks[i] = recover(addresses[i], false);  // on this pool thread
+      }
     } catch (Error&) {
       errs[i] = std::current_exception();
     }
@@ -1401,12 +1583,17 @@ void ErasureConsensus::_remove(const Address& a, const RemoveSignature& rs) {
     }
     nodes_.update(a, old, {});
   } else {
-    for (auto& nd : overlay_.lookup(a, total)) targets.push_back({nd.get(), -1});
+    // No placement of the block here (another client stored it, or a
+    // restart without rescan): every node is asked for every shard.  The
+    // shards may sit past lookup(a, k+m) -- stored while top-ranked nodes
+    // were down, or moved by a repair -- so the scan covers the whole
+    // membership, as remove_many reaches every peer that holds the block.
+    for (auto& nd : overlay_.lookup(a, (int)overlay_.size())) targets.push_back({nd.get(), -1});
   }
   std::atomic<int> removed{0};
   std::mutex emu;
   std::string refused;
-  std::vector<std::pair<Address, Key>> deferred;  // holders down now
+  std::vector<std::pair<Address, OwedRemove>> deferred;  // holders down now
   pool_.parallel_for(targets.size(), [&](size_t t) {
     Node* nd = targets[t].node;
     const int i0 = targets[t].index < 0 ? 0 : targets[t].index;
@@ -1432,18 +1619,20 @@ void ErasureConsensus::_remove(const Address& a, const RemoveSignature& rs) {
         nd->remove(key);
         ++removed;
       } catch (Unavailable&) {
-        // the node is down: remove its shard when it returns (or drop the
-        // debt when it is evicted), so the block does not come back with it
-        if (known) {
-          std::lock_guard<std::mutex> g(emu);
-          deferred.emplace_back(nd->id, key);
-        }
-        if (targets[t].index < 0) break;
+        // the node is down: remove its shard(s) when it returns (or drop
+        // the debt when it is evicted), so the block does not come back with
+        // it.  For a block of unknown placement, every index it might hold.
+        std::lock_guard<std::mutex> g(emu);
+        for (int j = i; j < i1; ++j) deferred.push_back({nd->id, OwedRemove{a, j}});
+        break;
       } catch (silo::MissingKey&) {
       }
     }
   });
-  if (!deferred.empty()) {
+  // owed removals: a known block's down holders; for a block of unknown
+  // placement, the down nodes' possible shards once the removal took
+  // effect somewhere (an address found nowhere owes nothing)
+  if (!deferred.empty() && (known || removed.load() > 0)) {
     std::lock_guard<std::mutex> g(rm_mu_);
     for (auto& d : deferred) pending_rm_[d.first].push_back(d.second);
   }
@@ -1463,22 +1652,31 @@ size_t ErasureConsensus::pending_removes() const {
 // Shards a removal could not reach on `node` (down at the time): erased now
 // that it is back, or forgotten with its silo when it is evicted.
 void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
-  std::vector<Key> keys;
+  std::vector<OwedRemove> owed;
   {
     std::lock_guard<std::mutex> g(rm_mu_);
     auto it = pending_rm_.find(node);
     if (it == pending_rm_.end()) return;
-    keys.swap(it->second);
+    owed.swap(it->second);
     pending_rm_.erase(it);
   }
   if (evicted) return;
   auto nd = overlay_.node(node);
-  std::vector<Key> still;
-  for (auto& k : keys) {
+  std::vector<OwedRemove> still;
+  for (auto& r : owed) {
+    // the block was stored again with this node holding that shard (a CHB
+    // key is its content's): the shard is live, the debt is void
+    {
+      std::shared_lock<std::shared_mutex> g(index_mu_);
+      auto it = index_.find(r.block);
+      if (it != index_.end() && r.index < (int)it->second.holder.size() &&
+          it->second.holder[r.index] == node)
+        continue;
+    }
     try {
-      if (nd) nd->remove(k);
+      if (nd) nd->remove(shard_key(r.block, r.index));
     } catch (Unavailable&) {
-      still.push_back(k);  // down again
+      still.push_back(r);  // down again
     } catch (silo::MissingKey&) {
     }
   }
@@ -1725,7 +1923,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
             taken.insert(nd->id);
             ++placed[t];
             break;
-          } catch (Unavailable&) {
+          } catch (Error&) {  // unreachable or full: the next candidate
           }
         }
         if (old && old != x.pl.holder[i]) {
@@ -2046,7 +2244,8 @@ void ErasureConsensus::membership_loop() {
 
 // "erasure" configuration: {"type": "erasure", "data-shards": k,
 // "parity-shards": m, "backend-replication-factor": f, and optionally
-// "device", "batch-max", "eviction-delay" (s), "stage-mb", "threads"};
+// "device", "batch-max", "eviction-delay" (s), "stage-mb", "threads",
+// "fetch-hedge", "verify-subsets"};
 // kebab-case keys as "replication-factor" (Paxos.cc:2273-2276).
 namespace {
 struct RegisterErasure {
@@ -2062,10 +2261,13 @@ struct RegisterErasure {
       o.device = get("device", 0);
       o.batch_max = get("batch-max", 256);
       o.eviction_delay_ms = (int64_t)get("eviction-delay", 600) * 1000;  // seconds
-      o.stage_bytes = (size_t)get("stage-mb", (int)(kStageBytes >> 20)) << 20;
+      const int stage_mb = get("stage-mb", (int)(kStageBytes >> 20));
       o.threads = get("threads", o.threads);
-      if (o.batch_max < 1 || o.stage_bytes == 0 || o.threads < 1)
+      o.fetch_hedge = get("fetch-hedge", o.fetch_hedge);
+      o.verify_subsets = get("verify-subsets", o.verify_subsets);
+      if (o.batch_max < 1 || stage_mb < 1 || o.threads < 1)
         throw Error("erasure: batch-max, stage-mb and threads must be positive");
+      o.stage_bytes = (size_t)stage_mb << 20;
       const int f = get("backend-replication-factor", 3);
       return std::unique_ptr<Consensus>(
           new ErasureConsensus(std::make_unique<ReplicationConsensus>(ov, f), ov, o));

@@ -158,6 +158,13 @@ constexpr size_t kStageBytes = (size_t)512 << 20;
 //   124 u32 crc32c(bytes 0..123 || payload)
 // The checksum covers the header too: a damaged size, salt or owner makes
 // the shard an erasure, not a poisoned reassembly.
+// A block reassembled from shards that each passed their CRC but together
+// do not hash to the block's address (a holder served a well-framed shard
+// with the wrong bytes).  Still a ValidationFailed to callers.
+struct AddressMismatch : ValidationFailed {
+  using ValidationFailed::ValidationFailed;
+};
+
 struct ShardHeader {
   static constexpr size_t kSize = 128;
   static constexpr uint8_t kVersion = 2;
@@ -276,6 +283,19 @@ struct ErasureOptions {
   // Rebuild under-placed blocks' missing shards onto newly discovered nodes
   // (rebalance_auto_expand, Paxos.cc:1149-1244).
   bool auto_expand = true;
+  // A degraded fetch asks for as many parity shards as the decode needs,
+  // plus this many more on its first round ("fetch-hedge": a slow or
+  // failing holder then costs no second round trip).
+  int fetch_hedge = 0;
+  // Parity holders are asked in order of in-flight transfers from this
+  // client, shuffled first (Paxos.cc:488-500); false when the environment
+  // sets INFINIT_DISABLE_BALANCED_TRANSFERS, as the reference reads it.
+  bool balanced_transfers = true;
+  // A reassembled block that fails its CHB address (a shard with a valid
+  // CRC but wrong bytes) is retried from other k-subsets of every reachable
+  // shard, at most this many ("verify-subsets"); the shards that disagree
+  // with the verified block are rewritten.  0: fail at once.
+  int verify_subsets = 64;
 };
 
 class ErasureConsensus : public StackedConsensus {
@@ -392,8 +412,14 @@ class ErasureConsensus : public StackedConsensus {
   std::exception_ptr place_batch(const std::vector<const Block*>& bs, const uint8_t* data,
                                  const uint8_t* parity, size_t S, std::vector<Placed>& placed);
   void batcher_loop();
+  // from (k + m entries): the node each gathered shard came from
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
-                                                    ShardHeader* hdr, bool parallel = true);
+                                                    ShardHeader* hdr, bool parallel = true,
+                                                    std::vector<Node*>* from = nullptr);
+  // A block whose reassembly failed its address, from another k-subset of
+  // its reachable shards; the disagreeing shards rewritten (AddressMismatch
+  // when no subset within verify_subsets matches).
+  std::unique_ptr<Block> recover(const Address& a, bool parallel);
   // index_ updates under index_mu_ (held exclusively by the caller); they
   // return the block's previous holders for the node index, which the
   // caller updates after releasing the lock
@@ -439,9 +465,27 @@ class ErasureConsensus : public StackedConsensus {
   int sub_token_ = -1;
   std::thread mthread_;
   std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0}, evictions_{0};
+  // reassemblies that failed their address and were recovered from another
+  // k-subset; shards found wrong that way and rewritten
+  std::atomic<uint64_t> subset_recoveries_{0}, corrupt_rewritten_{0};
   const OwnerDirectory* owners_ = nullptr;
   mutable std::mutex rm_mu_;
-  std::map<Address, std::vector<Key>> pending_rm_;  // node -> shard keys still to erase
+  // Shard removals owed to a node that was down: the block and shard index
+  // (so a returning node keeps a shard the block was stored again with)
+  struct OwedRemove {
+    Address block;
+    int index;
+  };
+  std::map<Address, std::vector<OwedRemove>> pending_rm_;  // node -> removals still owed
+  // in-flight fetches from this client per node (the reference's
+  // Paxos::_transfers), hashed into padded slots
+  struct alignas(64) TransferSlot {
+    std::atomic<int> n{0};
+  };
+  mutable std::array<TransferSlot, 64> transfers_;
+  std::atomic<int>& transfers(const Node* nd) const {
+    return transfers_[(reinterpret_cast<uintptr_t>(nd) >> 6) % transfers_.size()].n;
+  }
 };
 
 }  // namespace memo_host

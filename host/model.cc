@@ -123,10 +123,30 @@ std::optional<OwnerAcl> OwnerDirectory::find(const Address& owner) const {
   return it->second;
 }
 
+void OwnerDirectory::set_group(const Buffer& group_key, std::vector<Buffer> public_keys) {
+  std::lock_guard<std::mutex> g(mu_);
+  groups_[group_key] = std::move(public_keys);
+}
+
+std::optional<std::vector<Buffer>> OwnerDirectory::group_public_keys(const Buffer& group_key) const {
+  std::lock_guard<std::mutex> g(mu_);
+  auto it = groups_.find(group_key);
+  if (it == groups_.end()) return std::nullopt;
+  return it->second;
+}
+
 RemoveSignature chb_sign_remove(const Address& chb, const KeyPair& keys) {
   RemoveSignature rs;
   rs.signature_key = keys.public_key;
   rs.signature = keys.sign(chb.value.data(), chb.value.size());
+  return rs;
+}
+
+RemoveSignature chb_sign_remove_group(const Address& chb, const Buffer& group_key,
+                                      const KeyPair& current, int version) {
+  RemoveSignature rs = chb_sign_remove(chb, current);
+  rs.group_key = group_key;
+  rs.group_index = version - 1;
   return rs;
 }
 
@@ -140,8 +160,19 @@ std::string chb_validate_remove(const Address& chb, const Address& owner,
   const std::optional<OwnerAcl> acl = dir ? dir->find(owner) : std::nullopt;
   if (!acl) return "";  // owner block not found: allowed, as CHB.cc:222-227
   if (acl->world_write || acl->owner_key == key) return "";
-  for (auto& w : acl->writers)
-    if (w == key) return "";
+  if (!rs.group_key) {
+    for (auto& w : acl->writers)
+      if (w == key) return "";
+    return "Key not found";
+  }
+  // CHB.cc:243-258: the group's ACL entry must grant write, and the signing
+  // key must be the group's key of version group_index + 1
+  auto ge = std::find_if(acl->groups.begin(), acl->groups.end(),
+                         [&](const GroupAclEntry& e) { return e.group_key == *rs.group_key; });
+  if (ge == acl->groups.end() || !ge->write || !rs.group_index || !dir) return "Key not found";
+  const auto pubs = dir->group_public_keys(*rs.group_key);
+  const int gi = *rs.group_index;
+  if (pubs && gi >= 0 && gi < (int)pubs->size() && (*pubs)[gi] == key) return "";
   return "Key not found";
 }
 

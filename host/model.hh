@@ -143,42 +143,65 @@ bool verify_signature(const Buffer& public_key, const Buffer& signature, const u
                       size_t n);
 
 // blocks::RemoveSignature (src/memo/model/blocks/Block.hh:21-35): the key
-// that signed the removal and its signature of the block address.  The
-// group fields (group_key, group_index) are left out: groups are mutable
-// ACL blocks, outside this path.
+// that signed the removal and its signature of the block address; for a
+// removal signed through a group, the group's key and the index of the
+// group key version that signed (group_public_keys()[group_index] is
+// signature_key, CHB.cc:243-258).
 struct RemoveSignature {
+  std::optional<Buffer> group_key;
+  std::optional<int> group_index;
   std::optional<Buffer> signature_key;
   std::optional<Buffer> signature;
 };
 
 // What CHB::_validate_remove reads from a CHB's owner block, an ACB
 // (CHB.cc:203-259): the owner key, the keys with write access (ACL
-// entries) and the world-write permission.  model.fetch(owner) is restated
-// as a directory the network's clients share.
+// entries), the group entries (acl_group_entries: a group key and whether
+// the group may write) and the world-write permission.  model.fetch(owner)
+// is restated as a directory the network's clients share.
+struct GroupAclEntry {
+  Buffer group_key;
+  bool write = false;
+};
 struct OwnerAcl {
   Buffer owner_key;
   std::vector<Buffer> writers;
   bool world_write = false;
+  std::vector<GroupAclEntry> groups;
 };
+// The directory also restates the group blocks a removal names
+// (Group(dht, key).group_public_keys(), doughnut/Group.cc): per group key,
+// the public key of every version, oldest first (version v at index v - 1).
 class OwnerDirectory {
  public:
   void set(const Address& owner, OwnerAcl acl);
   std::optional<OwnerAcl> find(const Address& owner) const;
+  void set_group(const Buffer& group_key, std::vector<Buffer> public_keys);
+  std::optional<std::vector<Buffer>> group_public_keys(const Buffer& group_key) const;
 
  private:
   mutable std::mutex mu_;
   std::map<Address, OwnerAcl> acl_;
+  std::map<Buffer, std::vector<Buffer>> groups_;
 };
 
 // CHB::sign_remove (CHB.cc:140-201): `keys` sign the block address.
 RemoveSignature chb_sign_remove(const Address& chb, const KeyPair& keys);
+// CHB::sign_remove's group branch (CHB.cc:170-186): the group's current
+// key pair (version `version`, 1-based) signs, and the signature names the
+// group and the key's index (version - 1).
+RemoveSignature chb_sign_remove_group(const Address& chb, const Buffer& group_key,
+                                      const KeyPair& current, int version);
 // CHB::_validate_remove (CHB.cc:203-259) of a CHB at `chb` owned by `owner`:
 // "" when the removal is allowed, else the failure reason.  No owner:
 // allowed.  Owner set: the signature fields must be present ("Missing field
 // in signature") and verify over the address ("Invalid signature"); an
 // owner block the directory does not know is allowed (the reference warns
-// and allows, CHB.cc:222-227); else the key must be the owner's, a writer's,
-// or the block world-writable ("Key not found").
+// and allows, CHB.cc:222-227); else the block is world-writable, or the key
+// is the owner's, or -- without a group in the signature -- a writer's, or
+// -- with one -- the group has a write entry and its key of index
+// group_index is the signing key ("Key not found" otherwise; an unknown
+// group or a missing / out-of-range index is refused).
 std::string chb_validate_remove(const Address& chb, const Address& owner,
                                 const RemoveSignature& rs, const OwnerDirectory* dir);
 

@@ -324,7 +324,7 @@ TEST(chb_remove_validation_rules, false) {
   Block b = make_chb(bytes("owned"), bytes("s"), owner);
   Block free_b = make_chb(bytes("unowned"));
   OwnerDirectory dir;
-  dir.set(owner, OwnerAcl{owner_k.public_key, {writer_k.public_key}, false});
+  dir.set(owner, OwnerAcl{owner_k.public_key, {writer_k.public_key}, false, {}});
   // no owner: anyone, signed or not
   CHECK(chb_validate_remove(free_b.address, free_b.owner, {}, &dir).empty());
   // owned: the fields must be there and the signature must verify
@@ -341,12 +341,65 @@ TEST(chb_remove_validation_rules, false) {
   CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, writer_k), &dir).empty());
   CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), &dir) ==
         "Key not found");
-  dir.set(owner, OwnerAcl{owner_k.public_key, {}, true});  // world-writable
+  dir.set(owner, OwnerAcl{owner_k.public_key, {}, true, {}});  // world-writable
   CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), &dir).empty());
   // an owner block nobody knows: allowed once the signature verifies (the
   // reference warns and allows, CHB.cc:222-227)
   CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, other_k), nullptr).empty());
   CHECK(chb_validate_remove(b.address, owner, {}, nullptr) == "Missing field in signature");
+}
+
+// CHB::_validate_remove's group branch (CHB.cc:243-258) and
+// CHB::sign_remove's group signature (CHB.cc:170-186): a member removes an
+// owned CHB with the key of a group that has write access on the owner.
+TEST(chb_remove_group_key_rules, false) {
+  const KeyPair owner_k = KeyPair::generate(), g1 = KeyPair::generate(), g2 = KeyPair::generate(),
+                member_k = KeyPair::generate();
+  const Buffer G = KeyPair::generate().public_key, H = KeyPair::generate().public_key;
+  const Address owner = Address::random(flags::mutable_block);
+  Block b = make_chb(bytes("group owned"), bytes("s"), owner);
+  OwnerDirectory dir;
+  dir.set_group(G, {g1.public_key, g2.public_key});  // versions 1 and 2
+  dir.set_group(H, {g1.public_key});
+  OwnerAcl acl{owner_k.public_key, {member_k.public_key}, false, {{G, true}, {H, false}}};
+  dir.set(owner, acl);
+  // the group's current key (version 2, index 1) and its first one (index 0)
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, g2, 2), &dir).empty());
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, g1, 1), &dir).empty());
+  // the index must name the signing key's version
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, g2, 1), &dir) ==
+        "Key not found");
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, g2, 3), &dir) ==
+        "Key not found");
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, g2, 0), &dir) ==
+        "Key not found");
+  RemoveSignature no_index = chb_sign_remove_group(b.address, G, g2, 2);
+  no_index.group_index.reset();
+  CHECK(chb_validate_remove(b.address, owner, no_index, &dir) == "Key not found");
+  // a group entry without write access, a group not in the ACL, a group the
+  // network does not know
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, H, g1, 1), &dir) ==
+        "Key not found");
+  const Buffer U = KeyPair::generate().public_key;
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, U, g1, 1), &dir) ==
+        "Key not found");
+  acl.groups.push_back({U, true});
+  dir.set(owner, acl);
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, U, g1, 1), &dir) ==
+        "Key not found");
+  // with a group in the signature the individual entries are not consulted
+  // (CHB.cc:234-241 runs only without one): a writer signing "through" a
+  // group it is no key of is refused, and the same key signing alone passes
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, G, member_k, 2), &dir) ==
+        "Key not found");
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove(b.address, member_k), &dir).empty());
+  // the owner key passes with or without a group
+  CHECK(chb_validate_remove(b.address, owner, chb_sign_remove_group(b.address, H, owner_k, 1), &dir)
+            .empty());
+  // the signature must still verify
+  RemoveSignature bad = chb_sign_remove_group(b.address, G, g2, 2);
+  (*bad.signature)[0] ^= 1;
+  CHECK(chb_validate_remove(b.address, owner, bad, &dir) == "Invalid signature");
 }
 
 // The pinned arena keeps a few batch buffers for reuse, never one larger
@@ -393,7 +446,7 @@ TEST(remove_owned_chb_semantics, true) {
   OwnerDirectory dir;
   const KeyPair owner_k = KeyPair::generate(), other_k = KeyPair::generate();
   const Address owner = Address::random(flags::mutable_block);
-  dir.set(owner, OwnerAcl{owner_k.public_key, {}, false});
+  dir.set(owner, OwnerAcl{owner_k.public_key, {}, false, {}});
   net.ec->set_owner_directory(&dir);
   Block b = make_chb(random_bytes(70000, 77), bytes("salt"), owner);
   net.ec->store(b);
@@ -818,6 +871,241 @@ TEST(corrupted_shards_are_erasures, true) {
     }
   CHECK(flipped == 4);
   CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+namespace {
+// Shard i of `a` on whichever node holds it, re-framed with a valid header
+// and CRC around `payload_xor`-damaged bytes: the holder serves a shard
+// that passes every per-shard check but has the wrong bytes.
+bool reframe_shard(Net& net, const Address& a, int i, uint8_t payload_xor) {
+  const Key key = shard_key(a, i);
+  for (auto& n : net.nodes) {
+    if (!n->has(key)) continue;
+    Buffer w = n->silo->get(key);
+    const uint8_t* pay = nullptr;
+    const ShardHeader h = decode_shard(w, &pay);
+    Buffer bad(pay, pay + h.shard_size);
+    for (size_t x = 0; x < bad.size(); x += 61) bad[x] ^= payload_xor;
+    n->silo->set(key, encode_shard(h, bad.data(), i), false, true);
+    return true;
+  }
+  return false;
+}
+uint64_t stat(ErasureConsensus& ec, const char* key) {
+  return std::stoull(from_json(ec.stats())[key]);
+}
+int64_t total_fetches(const Net& net) {
+  int64_t f = 0;
+  for (auto& n : net.nodes) f += n->fetches.load();
+  return f;
+}
+}  // namespace
+
+// A shard with a valid CRC but wrong payload (a buggy holder re-framing, a
+// stale shard under a matching header) makes the reassembly fail its CHB
+// address.  The reference would move on to the next replica
+// (Paxos.cc:502-517); here the other k-subsets of the reachable shards
+// out-vote the wrong one, the fetch returns the exact bytes, and the bad
+// shard is rewritten on its holder.  m + 1 wrong shards leave no good
+// subset: ValidationFailed.
+TEST(reframed_shard_recovered_by_subset_retry, true) {
+  Net net(16, 10, 4);
+  Block b = make_chb(random_bytes(300000, 61)), c = make_chb(random_bytes(90000, 62));
+  net.ec->store(b);
+  net.ec->store(c);
+  // a data shard: the first attempt decodes nothing and fails the address
+  CHECK(reframe_shard(net, b.address, 3, 0xa5));
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+  CHECK(stat(*net.ec, "subset_recoveries") == 1);
+  CHECK(stat(*net.ec, "corrupt_shards_rewritten") == 1);
+  CHECK(net.ec->fetch(b.address)->data == b.data);  // repaired: no second recovery
+  CHECK(stat(*net.ec, "subset_recoveries") == 1);
+  // a parity shard used by a degraded decode, through the multi-fetch
+  std::shared_ptr<Node> d0;
+  for (auto& n : net.nodes)
+    if (n->has(shard_key(c.address, 0))) d0 = n;
+  CHECK(d0 != nullptr);
+  for (int i = 10; i < 14; ++i) CHECK(reframe_shard(net, c.address, i, 0x3c));
+  net.overlay.set_up(d0->id, false);
+  // four wrong parity shards and one data shard out of reach: 13 shards in
+  // hand, every k-subset holds a wrong one -- refused, not returned
+  CHECK_THROW(net.ec->fetch(c.address), ValidationFailed);
+  net.overlay.set_up(d0->id, true);
+  // with the data holder back, the multi-fetch reassembles from the data
+  // shards, needing no parity
+  int got = 0;
+  net.ec->fetch(std::vector<Address>{c.address, b.address},
+                [&](const Address& a, std::unique_ptr<Block> blk, std::exception_ptr e) {
+                  if (!e && blk && blk->data == (a == c.address ? c.data : b.data)) ++got;
+                });
+  CHECK(got == 2);
+  // one wrong parity shard in a degraded multi-fetch: recovered on the pool
+  Block d = make_chb(random_bytes(120000, 63));
+  net.ec->store(d);
+  std::shared_ptr<Node> dd;
+  for (auto& n : net.nodes)
+    if (n->has(shard_key(d.address, 5))) dd = n;
+  // parities 11-13 wrong, 10 right: whichever parity the decode took, the
+  // block comes back (a recovery when it was a wrong one)
+  for (int i = 11; i < 14; ++i) CHECK(reframe_shard(net, d.address, i, 0x11));
+  net.overlay.set_up(dd->id, false);
+  for (int r = 0; r < 4; ++r) {
+    got = 0;
+    net.ec->fetch(std::vector<Address>{d.address},
+                  [&](const Address&, std::unique_ptr<Block> blk, std::exception_ptr e) {
+                    if (!e && blk && blk->data == d.data) ++got;
+                  });
+    CHECK(got == 1);
+    CHECK(net.ec->fetch(d.address)->data == d.data);
+  }
+  net.overlay.set_up(dd->id, true);
+  // m + 1 = 5 wrong shards: no k-subset reassembles to the address
+  Block e5 = make_chb(random_bytes(50000, 64));
+  net.ec->store(e5);
+  for (int i : {0, 2, 4, 11, 13}) CHECK(reframe_shard(net, e5.address, i, 0x77));
+  CHECK_THROW(net.ec->fetch(e5.address), ValidationFailed);
+}
+
+// A degraded fetch reads only what the decode needs: with one data holder
+// down, k shard reads (9 data + 1 parity) instead of every parity shard,
+// plus the configured hedge; the parity holders asked vary from fetch to
+// fetch (shuffled, least-loaded first, Paxos.cc:488-500), and with the
+// balancing off the first parity holder is always asked.
+TEST(degraded_fetch_reads_k_shards, true) {
+  for (int hedge : {0, 1}) {
+    for (bool balanced : {true, false}) {
+      Net net(16, 10, 4);
+      net.o.fetch_hedge = hedge;
+      net.o.balanced_transfers = balanced;
+      net.restart();
+      Block b = make_chb(random_bytes(200000, 70 + hedge));
+      net.ec->store(b);
+      std::shared_ptr<Node> d2;
+      std::map<int, std::shared_ptr<Node>> parity_holder;
+      for (auto& n : net.nodes)
+        for (int i = 0; i < 14; ++i)
+          if (n->has(shard_key(b.address, i))) {
+            if (i == 2) d2 = n;
+            if (i >= 10) parity_holder[i] = n;
+          }
+      CHECK(d2 && parity_holder.size() == 4);
+      // healthy: the k data shards only
+      int64_t f0 = total_fetches(net);
+      CHECK(net.ec->fetch(b.address)->data == b.data);
+      CHECK(total_fetches(net) - f0 == 10);
+      net.overlay.set_up(d2->id, false);
+      std::set<int> asked;
+      for (int r = 0; r < 24; ++r) {
+        std::map<int, int64_t> before;
+        for (auto& [i, n] : parity_holder) before[i] = n->fetches.load();
+        f0 = total_fetches(net);
+        CHECK(net.ec->fetch(b.address)->data == b.data);
+        CHECK(total_fetches(net) - f0 == 10 + hedge);
+        for (auto& [i, n] : parity_holder)
+          if (n->fetches.load() > before[i]) asked.insert(i);
+      }
+      if (balanced) CHECK(asked.size() >= 3);
+      else CHECK(asked.size() == (size_t)(1 + hedge) && asked.count(10) == 1);
+      net.overlay.set_up(d2->id, true);
+    }
+  }
+}
+
+// A silo that refuses a shard (silo::InsufficientSpace) fails that shard
+// only: the batch's other shards are stored and every stored shard is in
+// the placement index (nothing orphaned in a silo), the blocks read back.
+TEST(full_silo_fails_only_its_shards, true) {
+  Net net(15, 10, 4);
+  uint8_t id[32] = {0};
+  id[0] = 0xf0;
+  id[1] = 0x11;
+  net.nodes.push_back(net.overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>(3000)));
+  net.o.auto_expand = false;
+  net.restart();
+  std::vector<Block> blocks;
+  for (int i = 0; i < 64; ++i) blocks.push_back(make_chb(random_bytes(60000 + 13 * i, 400 + i)));
+  net.ec->store_many(blocks);
+  size_t indexed = 0, on_silos = 0;
+  for (auto& n : net.nodes) indexed += net.ec->node_blocks(n->id);
+  for (auto& b : blocks) {
+    on_silos += net.holders(b.address, 14);
+    CHECK(net.ec->fetch(b.address)->data == b.data);
+  }
+  CHECK(indexed == on_silos);
+  CHECK(net.nodes.back()->silo->usage() == 0);  // every shard is > 3000 bytes
+  CHECK(net.ec->under_placed() > 0);             // the blocks it was to hold
+}
+
+// A client with no placement of a block removes every shard of it, also
+// shards on nodes ranked past k + m (stored while top-ranked nodes were
+// down), by asking the whole membership.
+TEST(remove_unknown_block_reaches_every_holder, true) {
+  Net net(16, 10, 4);
+  net.o.auto_expand = false;
+  net.restart();
+  Block b = make_chb(random_bytes(30000, 80));
+  auto rank = net.overlay.rank(b.address);
+  net.overlay.set_up(rank[0]->id, false);
+  net.overlay.set_up(rank[1]->id, false);
+  net.ec->store(b);
+  net.overlay.set_up(rank[0]->id, true);
+  net.overlay.set_up(rank[1]->id, true);
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK(!rank[0]->has(shard_key(b.address, 0)));
+  ErasureOptions o = net.o;
+  o.rescan = false;
+  ErasureConsensus other(std::make_unique<ReplicationConsensus>(net.overlay, 3), net.overlay, o);
+  other.remove(b.address);
+  CHECK(net.shards(b.address, 14) == 0);
+}
+
+// A removal owed to a holder that was down is void when the block was
+// stored again with that holder holding the shard before the node's return
+// was processed: the live shard stays.
+TEST(owed_removal_spares_restored_shard, true) {
+  Net net(16, 10, 4);
+  net.o.auto_expand = false;
+  net.restart();
+  Block b = make_chb(random_bytes(45000, 81));
+  net.ec->store(b);
+  std::shared_ptr<Node> h;
+  for (auto& n : net.nodes)
+    if (n->has(shard_key(b.address, 4))) h = n;
+  CHECK(h != nullptr);
+  net.overlay.set_up(h->id, false);
+  net.ec->remove(b.address);
+  CHECK(net.ec->pending_removes() == 1);
+  h->up = true;  // back, its return not yet signalled
+  net.ec->store(b);
+  CHECK(h->has(shard_key(b.address, 4)) && net.shards(b.address, 14) == 14);
+  h->up = false;
+  net.overlay.set_up(h->id, true);  // the return: owed removals settle
+  CHECK(wait_for([&] { return net.ec->pending_removes() == 0; }));
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  CHECK(net.shards(b.address, 14) == 14);
+  CHECK(net.ec->fetch(b.address)->data == b.data);
+}
+
+// CHB.cc:243-258 through the plugin: a group member's removal of a CHB whose
+// owner grants the group write access takes every shard; a group without
+// write access is refused with every shard left.
+TEST(remove_owned_chb_by_group_member, true) {
+  Net net(16, 10, 4);
+  OwnerDirectory dir;
+  const KeyPair owner_k = KeyPair::generate(), g1 = KeyPair::generate(), g2 = KeyPair::generate();
+  const Buffer G = KeyPair::generate().public_key, R = KeyPair::generate().public_key;
+  const Address owner = Address::random(flags::mutable_block);
+  dir.set_group(G, {g1.public_key});
+  dir.set_group(R, {g2.public_key});
+  dir.set(owner, OwnerAcl{owner_k.public_key, {}, false, {{G, true}, {R, false}}});
+  net.ec->set_owner_directory(&dir);
+  Block b = make_chb(random_bytes(33000, 82), bytes("salt"), owner);
+  net.ec->store(b);
+  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove_group(b.address, R, g2, 1)), ValidationFailed);
+  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove_group(b.address, G, g1, 2)), ValidationFailed);
+  CHECK(net.shards(b.address, 14) == 14);
+  net.ec->remove(b.address, chb_sign_remove_group(b.address, G, g1, 1));
+  CHECK(net.shards(b.address, 14) == 0);
 }
 
 // tests/doughnut.cc:1651-1691 (evict_faulty), 1484-1512 (expand_new_block),

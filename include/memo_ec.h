@@ -138,8 +138,18 @@ enum memo_ec_option {
                                            column-per-lane kernel (65536)        */
     MEMO_EC_OPT_DECODE_EXACT = 9,       /* MEMO_EC_DECODE_EXACT: exact-k decode
                                            kernels (1)                           */
-    MEMO_EC_OPT_DECODE_STAGE = 10       /* MEMO_EC_DECODE_STAGE: decode rows staged
+    MEMO_EC_OPT_DECODE_STAGE = 10,      /* MEMO_EC_DECODE_STAGE: decode rows staged
                                            through LDS (0)                       */
+    MEMO_EC_OPT_IMAGE_MIN_TILES = 11,   /* MEMO_EC_IMAGE_MIN_TILES: the decode rows +
+                                           MAC rebuild forms per-block product-
+                                           table images in HBM for blocks of at
+                                           least this many 4 KiB shard tiles and
+                                           runs the encode body over them
+                                           (2; 0: never, tables built in LDS)    */
+    MEMO_EC_OPT_IMAGE_MIN_COEFS = 12    /* MEMO_EC_IMAGE_MIN_COEFS: ... and at least
+                                           this many coefficients per block
+                                           (padded rows x columns; 56) or a k
+                                           without a straight-line MAC body      */
 };
 
 /* Number of GPUs the library can use (0 without a GPU).  A node process

@@ -36,6 +36,8 @@ struct memo_ec_opts {
   uint64_t decode_wide_max = 65536;       // column-per-lane decode up to this many blocks
   int decode_exact = 1;
   int decode_stage = 0;
+  uint64_t image_min_tiles = 2;           // rows path: HBM table images from this many tiles/block
+  uint64_t image_min_coefs = 56;          //   and this many coefficients per block (R x kpad)
 };
 
 struct memo_ec_ctx {
@@ -155,6 +157,14 @@ bool set_opt(memo_ec_opts& o, int opt, int64_t v) {
       if (v < 0 || v > 1) return false;
       o.decode_stage = (int)v;
       return true;
+    case MEMO_EC_OPT_IMAGE_MIN_TILES:
+      if (v < 0) return false;
+      o.image_min_tiles = (uint64_t)v;
+      return true;
+    case MEMO_EC_OPT_IMAGE_MIN_COEFS:
+      if (v < 0) return false;
+      o.image_min_coefs = (uint64_t)v;
+      return true;
     default:
       return false;
   }
@@ -172,6 +182,8 @@ bool get_opt(const memo_ec_opts& o, int opt, int64_t* v) {
     case MEMO_EC_OPT_DECODE_WIDE_MAX: *v = (int64_t)o.decode_wide_max; return true;
     case MEMO_EC_OPT_DECODE_EXACT: *v = o.decode_exact; return true;
     case MEMO_EC_OPT_DECODE_STAGE: *v = o.decode_stage; return true;
+    case MEMO_EC_OPT_IMAGE_MIN_TILES: *v = (int64_t)o.image_min_tiles; return true;
+    case MEMO_EC_OPT_IMAGE_MIN_COEFS: *v = (int64_t)o.image_min_coefs; return true;
     default: return false;
   }
 }
@@ -198,6 +210,8 @@ void read_env_options(memo_ec_opts& o) {
       {"MEMO_EC_DECODE_WIDE_MAX", MEMO_EC_OPT_DECODE_WIDE_MAX, 0},
       {"MEMO_EC_DECODE_EXACT", MEMO_EC_OPT_DECODE_EXACT, 0},
       {"MEMO_EC_DECODE_STAGE", MEMO_EC_OPT_DECODE_STAGE, 0},
+      {"MEMO_EC_IMAGE_MIN_TILES", MEMO_EC_OPT_IMAGE_MIN_TILES, 0},
+      {"MEMO_EC_IMAGE_MIN_COEFS", MEMO_EC_OPT_IMAGE_MIN_COEFS, 0},
   };
   for (const Env& e : kEnv) {
     const char* p = std::getenv(e.name);
@@ -612,11 +626,42 @@ DecodeArgs decode_args(const memo_ec_ctx* c, int k, int m, int e, size_t n, cons
   return a;
 }
 
+// Rows path: per-block product-table images through HBM (formed by the
+// decode, then gf_mac_kernel's encode body over them) when a block spans at
+// least the ctx's MEMO_EC_OPT_IMAGE_MIN_TILES tiles and its tables are
+// costly to build per tile: R x kpad >= MEMO_EC_OPT_IMAGE_MIN_COEFS, or k
+// off the straight-line bodies (the chunk loop builds its images one per
+// lane, after the barrier).  The LDS build inside the MAC is the right call
+// for small blocks (4 KiB RS(16,4): a 2 KiB image per 5 KiB of traffic,
+// DESIGN.md 4.1); a block of T tiles builds the same images T times there,
+// against one build and R * kpad * 32 bytes of HBM per block here.
+// Measured, interleaved on one box (tools/image_ab.py):
+// RS(16,4) 128 KiB-4 MiB +2.6 to +4 points, RS(8,4) / RS(20,4) / RS(10,6)
+// +3 to +5; RS(4,2), RS(6,3), RS(10,4), RS(12,4) -0.4 to 0 (kept in LDS);
+// one-tile blocks -0.1 (RS(16,4) 64 KiB) to -60 (4 KiB).
+bool rows_images(const memo_ec_ctx* c, size_t S, int k, int R, int KC) {
+  const uint64_t t = c->opt.image_min_tiles;
+  if (t == 0 || (S / 16 + MAC_TILE - 1) / MAC_TILE < t) return false;
+  return KC != k || (uint64_t)R * kpad_of((uint32_t)k, KC) >= c->opt.image_min_coefs;
+}
+size_t round256(size_t b) { return (b + 255) & ~(size_t)255; }
+// The decode of `a` also forms its rows' table images (R x kpad slots per
+// block) at img.
+void with_images(DecodeArgs& a, uint32_t* img, int R, int KC) {
+  a.img = img;
+  a.R = (uint32_t)R;
+  a.kpad = kpad_of(a.k, KC);
+}
+size_t image_bytes(size_t n, int k, int R, int KC) {
+  return n * (size_t)R * kpad_of((uint32_t)k, KC) * 32;
+}
+
 // Device-resident rebuild on stream st.  Fused (default): one launch of
 // gf_rebuild_kernel, whose tiles derive their blocks' decode rows from the
 // indices.  Two-kernel: closed-form decode rows (one lane per block) into
-// `scratch` (room for tab_bytes(k, e, n)), then the MAC, which builds each
-// block's product tables in LDS from its rows.  Faults go to `status`.
+// `scratch` (room for rebuild_scratch(...)), then the MAC, which builds each
+// block's product tables in LDS from its rows, or (rows_images) reads the
+// images rows_image_kernel formed behind the rows.  Faults go to `status`.
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
                    bool fused, void* scratch, hipStream_t st, uint32_t* status) {
@@ -644,23 +689,34 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
   const uint64_t row_b = (uint64_t)e * k;
   const uint32_t* lw0 = nullptr;
   if (int rc = lw0_table(ctx, k, m, &lw0)) return rc;
-  const DecodeArgs a = decode_args(ctx, k, m, e, n, surv_idx, lost_idx, rows, status, lw0);
+  DecodeArgs a = decode_args(ctx, k, m, e, n, surv_idx, lost_idx, rows, status, lw0);
+  const bool images = rows_images(ctx, S, k, R, KC);
+  uint32_t* img = reinterpret_cast<uint32_t*>(rows + round256(n * row_b));
+  const uint64_t img_dw = (uint64_t)R * kpad_of((uint32_t)k, KC) * 8;  // per block
+  if (images) with_images(a, img, R, KC);
   HIPCHK(launch_decode_coef(a, st));
   for (size_t b0 = 0; b0 < n; b0 += step) {
     const size_t cnt = std::min(step, n - b0);
-    std::vector<Plan> plans{plan_segment((uint32_t)k, (uint32_t)e, S, cnt,
-                                         surv + b0 * (size_t)k * S, (uint64_t)k * S, S,
-                                         out + b0 * (size_t)e * S, (uint64_t)e * S, S,
-                                         nullptr, 0, KC, R, rows + b0 * row_b, row_b,
-                                         (uint32_t)e)};
+    std::vector<Plan> plans{
+        images ? plan_segment((uint32_t)k, (uint32_t)e, S, cnt, surv + b0 * (size_t)k * S,
+                              (uint64_t)k * S, S, out + b0 * (size_t)e * S, (uint64_t)e * S, S,
+                              img + b0 * img_dw, img_dw, KC, R)
+               : plan_segment((uint32_t)k, (uint32_t)e, S, cnt, surv + b0 * (size_t)k * S,
+                              (uint64_t)k * S, S, out + b0 * (size_t)e * S, (uint64_t)e * S, S,
+                              nullptr, 0, KC, R, rows + b0 * row_b, row_b, (uint32_t)e)};
     if (int rc = launch_plans(ctx, plans, st)) return rc;
   }
   return MEMO_EC_OK;
 }
 
-// Rebuild scratch for n blocks: their decode rows, e x k bytes each (the
+// Rebuild scratch for n blocks (a multiple of 256 bytes): their decode rows,
+// e x k bytes each, and behind them (rows_images) their table images (the
 // two-kernel path; the fused one needs none).
-size_t tab_bytes(int k, int e, size_t n, bool fused) { return fused ? 0 : n * (size_t)e * k; }
+size_t rebuild_scratch(const memo_ec_ctx* c, int k, int e, size_t S, size_t n, bool fused) {
+  if (fused) return 0;
+  const int R = mac_rbound(e), KC = mac_kchunk(k, R);
+  return round256(n * (size_t)e * k) + (rows_images(c, S, k, R, KC) ? image_bytes(n, k, R, KC) : 0);
+}
 
 // Deferred-error words in ctx->d_status: device-resident calls (reported by
 // memo_ec_synchronize) and the host-memory copy pipeline (reported by the
@@ -891,15 +947,23 @@ struct RPiece {
   const uint8_t* lidx = nullptr;  // per-block: n x e
   uint8_t* out = nullptr;         // n x e x S
   int mode = MAC_ENCODE, KC = 4, R = 1;
+  bool img = false;               // MAC_ROWS: table images through HBM (rows_images)
   const uint32_t* tab = nullptr;  // shared pattern: table image
+  // the MAC launch this piece takes (MAC_ROWS with images: the encode body)
+  int mac_mode() const { return img ? MAC_ENCODE : mode; }
 };
 
-// Decode-row bytes the pieces of MAC_ROWS classes need.
-size_t rows_bytes(const std::vector<RPiece>& ps) {
-  size_t b = 0;
-  for (const auto& p : ps)
-    if (p.mode == MAC_ROWS) b += p.n * (size_t)p.e * p.k;
-  return b;
+// Scratch bytes (a multiple of 256) the MAC_ROWS pieces of `ps` need: the
+// decode rows of every piece, then the table images of the pieces with img.
+template <class Pieces>
+size_t rows_scratch(const Pieces& ps) {
+  size_t rows = 0, img = 0;
+  for (const RPiece& p : ps) {
+    if (p.mode != MAC_ROWS) continue;
+    rows += p.n * (size_t)p.e * p.k;
+    if (p.img) img += image_bytes(p.n, p.k, p.R, p.KC);
+  }
+  return round256(rows) + img;
 }
 
 // Validates the segments and assigns each non-empty one its class:
@@ -962,19 +1026,26 @@ int plan_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_segmen
       if (int rc = pattern_tables(c, p.k, p.m, p.sidx, p.lidx, p.e, p.R, p.KC, &p.tab)) return rc;
     } else {
       p.mode = rebuild_fused(c, k.in_bytes) ? MAC_FUSED : MAC_ROWS;
+      p.img = p.mode == MAC_ROWS && rows_images(c, p.S, p.k, p.R, p.KC);
     }
   }
   return MEMO_EC_OK;
 }
 
 // Enqueue the kernels of `ps` on st: decode rows of MAC_ROWS pieces into
-// `rows` (rows_bytes(ps) bytes), then one launch set per (mode, KC, R)
-// class, pieces longer than one launch's grid split by blocks.
+// `rows` (rows_scratch(ps) bytes: the rows, then the table images of the
+// pieces with img), then one launch set per (MAC mode, KC, R) class, pieces
+// longer than one launch's grid split by blocks.
 int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t* rows,
                           hipStream_t st, uint32_t* status) {
   std::vector<const uint8_t*> prow(ps.size(), nullptr);
+  std::vector<const uint32_t*> pimg(ps.size(), nullptr);
   std::vector<DecodeArgs> dec;
-  size_t off = 0;
+  size_t off = 0, rows_total = 0;
+  for (const auto& p : ps)
+    if (p.mode == MAC_ROWS) rows_total += p.n * (size_t)p.e * p.k;
+  uint8_t* img_base = rows + round256(rows_total);
+  size_t ioff = 0;
   for (size_t i = 0; i < ps.size(); ++i) {
     const auto& p = ps[i];
     if (p.mode != MAC_ROWS) continue;
@@ -982,18 +1053,25 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
     if (int rc = lw0_table(c, p.k, p.m, &lw0)) return rc;
     dec.push_back(decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0));
     prow[i] = rows + off;
+    if (p.img) {
+      uint32_t* img = reinterpret_cast<uint32_t*>(img_base + ioff);
+      pimg[i] = img;
+      with_images(dec.back(), img, p.R, p.KC);
+      ioff += image_bytes(p.n, p.k, p.R, p.KC);
+    }
     off += p.n * (size_t)p.e * p.k;
   }
-  // every segment's decode rows, segments of one decode kernel per launch
+  // every segment's decode rows (and table images), segments of one decode
+  // kernel per launch
   if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
   std::vector<bool> done(ps.size(), false);
   for (size_t i = 0; i < ps.size(); ++i) {
     if (done[i]) continue;
-    const int mode = ps[i].mode, KC = ps[i].KC, R = ps[i].R;
+    const int mode = ps[i].mac_mode(), KC = ps[i].KC, R = ps[i].R;
     std::vector<Plan> plans;
     for (size_t j = i; j < ps.size(); ++j) {
       const auto& p = ps[j];
-      if (done[j] || p.mode != mode || p.KC != KC || p.R != R) continue;
+      if (done[j] || p.mac_mode() != mode || p.KC != KC || p.R != R) continue;
       done[j] = true;
       const size_t step = max_blocks_per_launch(c, p.S);
       const uint32_t* lw0 = nullptr;
@@ -1004,7 +1082,11 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
         const uint64_t in_bs = (uint64_t)p.k * p.S, out_bs = (uint64_t)p.e * p.S;
         const uint8_t* in = p.surv + b0 * in_bs;
         uint8_t* out = p.out + b0 * out_bs;
-        if (mode == MAC_ENCODE) {
+        if (p.img) {
+          const uint64_t per_dw = (uint64_t)R * kpad_of((uint32_t)p.k, KC) * 8;
+          plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
+                                       p.S, pimg[j] + b0 * per_dw, per_dw, KC, R));
+        } else if (mode == MAC_ENCODE) {
           plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
                                        p.S, p.tab, 0, KC, R));
         } else if (mode == MAC_ROWS) {
@@ -1324,7 +1406,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   DeviceGuard g(c->device);
   const bool fused = rebuild_fused(c, n * (size_t)k * S);
   if (where == MEMO_EC_DEVICE) {
-    if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
+    if (int rc = ensure_tabs(c, rebuild_scratch(c, k, e, S, n, fused))) return rc;
     if (int rc = rebuild_device(c, k, m, S, n, surv_idx, surv, lost_idx, e, out, fused, c->d_tabs,
                                 c->stream, c->d_status + kStatusDevice))
       return rc;
@@ -1349,7 +1431,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
     // pinned buffers); the status word rides in the slot too.
     const size_t slot = n * (in_b + out_b + idx_b) + 64;
     if (int rc = ensure_slots(c, 0, slot)) return rc;
-    if (int rc = ensure_tabs(c, tab_bytes(k, e, n, fused))) return rc;
+    if (int rc = ensure_tabs(c, rebuild_scratch(c, k, e, S, n, fused))) return rc;
     uint8_t* h = c->h_slot[0];
     uint8_t* h_sidx = h + n * (in_b + out_b);
     uint8_t* h_lidx = h_sidx + n * k;
@@ -1382,7 +1464,7 @@ int memo_ec_rebuild_batch(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
   const size_t slot = nb * (in_b + out_b + idx_b);
   const size_t hshift = pinned ? nb * (in_b + out_b) : 0;  // host slot offset of the device layout
   if (int rc = ensure_slots(c, slot, slot - hshift)) return rc;
-  const size_t tabs = tab_bytes(k, e, nb, fused);
+  const size_t tabs = rebuild_scratch(c, k, e, S, nb, fused);
   if (int rc = ensure_tabs(c, kSlots * tabs)) return rc;
   const size_t o_out = nb * in_b, o_sidx = o_out + nb * out_b, o_lidx = o_sidx + nb * k;
   const int rc = run_pipeline(
@@ -1490,7 +1572,7 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
   if (int rc = plan_rebuild_segments(c, nseg, segs, ps)) return rc;
   if (ps.empty()) return MEMO_EC_OK;
   if (where == MEMO_EC_DEVICE) {
-    if (int rc = ensure_tabs(c, rows_bytes(ps))) return rc;
+    if (int rc = ensure_tabs(c, rows_scratch(ps))) return rc;
     if (int rc = launch_rebuild_pieces(c, ps, reinterpret_cast<uint8_t*>(c->d_tabs), c->stream,
                                        c->d_status + kStatusDevice))
       return rc;
@@ -1540,7 +1622,7 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
   }
   struct Wave {
     std::vector<size_t> ids;
-    size_t in = 0, out = 0, idx = 0, rows = 0;
+    size_t in = 0, out = 0, idx = 0;
   };
   std::vector<Wave> waves;
   const bool zc = total + 64 <= zc_max_bytes(c);
@@ -1551,7 +1633,6 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
     w.in += ch[i].in;
     w.out += ch[i].out;
     w.idx += ch[i].idx;
-    if (ch[i].p.mode == MAC_ROWS) w.rows += ch[i].p.n * (size_t)ch[i].p.e * ch[i].p.k;
   }
   size_t slot = 0, rows = 0;
   for (Wave& w : waves) {
@@ -1565,9 +1646,10 @@ int memo_ec_rebuild_segments(memo_ec_ctx* c, int nseg, const memo_ec_rebuild_seg
       ox += ch[i].idx;
     }
     slot = std::max(slot, w.in + w.out + w.idx);
-    rows = std::max(rows, w.rows);
+    std::vector<RPiece> wp;
+    for (size_t i : w.ids) wp.push_back(ch[i].p);
+    rows = std::max(rows, rows_scratch(wp));  // decode rows + table images (256-byte multiple)
   }
-  rows = (rows + 255) & ~(size_t)255;
   // the pieces as the kernels see them, in slot memory at base (surv / out
   // at the caller's pinned buffers when pinned_io)
   auto staged = [&](const Wave& w, uint8_t* base, bool pinned_io) {

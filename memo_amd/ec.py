@@ -54,7 +54,8 @@ class RebuildSegment(ctypes.Structure):
 # memo_ec_option (include/memo_ec.h)
 OPTIONS = {"rebuild_path": 1, "fused_max_bytes": 2, "zero_copy_bytes": 3, "pipe_bytes": 4,
            "copy_threads": 5, "max_launch_tiles": 6, "xcd_min_tiles": 7, "decode_wide_max": 8,
-           "decode_exact": 9, "decode_stage": 10}
+           "decode_exact": 9, "decode_stage": 10, "image_min_tiles": 11,
+           "image_min_coefs": 12}
 MAX_REBUILD_SEGMENTS = 256
 PROBE_MODES = {"copy": 0, "read": 1, "write": 2}  # memo_ec_probe_mode
 
@@ -187,7 +188,11 @@ def erasures(seed, first_block, n, k, m, e):
 
 
 REBUILD_KERNELS = {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
-                   "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM)"}
+                   "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM, "
+                           "tables built in LDS)",
+                   "images": "decode_coef*/decode_rows_k forming per-block table images "
+                             "(beside the rows, or by rows_image_kernel) + gf_mac_kernel "
+                             "encode body (images through HBM)"}
 
 
 def _is_torch(x):
@@ -281,19 +286,38 @@ class Codec:
                     self.set_option(k, v)
         return cm()
 
-    def rebuild_path(self, n, k, S):
+    def rebuild_path(self, n, k, S, e=None):
         """The device rebuild this ctx runs for n blocks of k survivor shards
         of S bytes (memo_ec.cpp rebuild_fused, from the ctx's options as set
         by the environment or set_option): 'fused' (one gf_rebuild_kernel
-        launch whose tiles derive their blocks' decode rows) or 'rows'
-        (decode rows through HBM, then gf_mac_kernel)."""
+        launch whose tiles derive their blocks' decode rows), 'rows'
+        (decode rows through HBM, then gf_mac_kernel building each tile's
+        tables in LDS) or 'images' (decode rows, then per-block table images
+        through HBM for blocks of >= image_min_tiles 4 KiB shard tiles with
+        costly tables (uses_images), then gf_mac_kernel's encode body).  e
+        (lost shards per block) defaults to 4."""
         path = self.get_option("rebuild_path")
-        if path >= 0:
-            return "fused" if path else "rows"
-        return "fused" if n * k * S <= self.get_option("fused_max_bytes") else "rows"
+        if path < 0:
+            path = 1 if n * k * S <= self.get_option("fused_max_bytes") else 0
+        if path:
+            return "fused"
+        return "images" if self.uses_images(k, S, e) else "rows"
 
-    def rebuild_kernel_name(self, n, k, S):
-        return REBUILD_KERNELS[self.rebuild_path(n, k, S)]
+    def uses_images(self, k, S, e=None):
+        """Whether the rows path forms per-block table images in HBM for
+        this geometry (memo_ec.cpp rows_images): blocks of >= image_min_tiles
+        4 KiB shard tiles whose R x kpad coefficients reach image_min_coefs,
+        or any k without a straight-line MAC body.  e defaults to 4."""
+        t = self.get_option("image_min_tiles")
+        if not t or -(-S // 4096) < t:
+            return False
+        R = mac_rbound(4 if e is None else e)
+        KC = mac_kchunk(k, R)
+        kpad = -(-k // KC) * KC
+        return KC != k or R * kpad >= self.get_option("image_min_coefs")
+
+    def rebuild_kernel_name(self, n, k, S, e=None):
+        return REBUILD_KERNELS[self.rebuild_path(n, k, S, e)]
 
     # -- codec
     def encode(self, k, m, data, parity, S=None, n=None):
@@ -427,6 +451,20 @@ class Codec:
         _check(_lib().memo_ec_gather_shards(self._ctx, k, m, S, n, _ptr(data)[0], _ptr(parity)[0],
                                             _ptr(idx)[0], cnt, _ptr(out)[0]), "gather_shards")
         return out
+
+
+def mac_rbound(r):
+    """Compile-time output-row bound of the MAC (ec_kernels.hip mac_rbound)."""
+    return r if r <= 4 else 6 if r <= 6 else 8 if r <= 8 else 12 if r <= 12 else 16
+
+
+def mac_kchunk(k, R):
+    """Straight-line shard chunk of the MAC (ec_kernels.hip mac_kchunk)."""
+    if k in (2, 3, 4, 10, 16):
+        return k
+    if k in (6, 12, 14):
+        return k if R <= 4 else 4
+    return 4
 
 
 def _check_pattern(si, li, k, m):

@@ -40,17 +40,23 @@ def codec():
     c.close()
 
 
-@pytest.fixture(params=["fused", "rows"])
+@pytest.fixture(params=["fused", "rows", "images"])
 def rebuild_path(request, monkeypatch):
-    """Run a rebuild test on both device rebuild paths: the fused
-    gf_rebuild_kernel (default) and the two-kernel decode_coef_kernel +
-    gf_mac_kernel path: the session codec's MEMO_EC_OPT_REBUILD_PATH, and
-    MEMO_EC_REBUILD_FUSED for contexts the test creates itself."""
+    """Run a rebuild test on every device rebuild path: the fused
+    gf_rebuild_kernel (default up to 256 MiB), the two-kernel decode rows +
+    gf_mac_kernel path with tables built in LDS ("rows", images off), and
+    the same with per-block table images through HBM for every block size
+    ("images", image_min_tiles 1, image_min_coefs 0): the session codec's
+    options, and MEMO_EC_REBUILD_FUSED / MEMO_EC_IMAGE_MIN_TILES /
+    MEMO_EC_IMAGE_MIN_COEFS for contexts the test creates itself."""
     v = 1 if request.param == "fused" else 0
+    t = 1 if request.param == "images" else 0
     monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", str(v))
+    monkeypatch.setenv("MEMO_EC_IMAGE_MIN_TILES", str(t))
+    monkeypatch.setenv("MEMO_EC_IMAGE_MIN_COEFS", "0")
     if "codec" in request.fixturenames:
         c = request.getfixturevalue("codec")
-        with c.options(rebuild_path=v):
+        with c.options(rebuild_path=v, image_min_tiles=t, image_min_coefs=0):
             yield request.param
     else:
         yield request.param

@@ -301,12 +301,12 @@ def test_block_beyond_32bit_offsets(codec, O):
     surv = empty(n, k * S)
     codec.gather_shards(k, m, S, n, d, p, dev(s), surv)
     del d, p
-    for path in (0, 1):
+    for path, img in ((0, 0), (0, 1), (1, 0)):
         out = empty(n, S)
-        with codec.options(rebuild_path=path):
+        with codec.options(rebuild_path=path, image_min_tiles=img, image_min_coefs=0):
             codec.rebuild(k, m, dev(s), surv, dev(l), out)
             codec.synchronize()
-        assert np.array_equal(host(out)[0], data[0, :S]), path
+        assert np.array_equal(host(out)[0], data[0, :S]), (path, img)
         del out
 
 
@@ -1025,7 +1025,8 @@ def test_ctx_options_round_trip(codec):
     from memo_amd import ec
     values = {"rebuild_path": 0, "fused_max_bytes": 1 << 20, "zero_copy_bytes": 0,
               "pipe_bytes": 8 << 20, "copy_threads": 2, "max_launch_tiles": 1000,
-              "xcd_min_tiles": 1, "decode_wide_max": 0, "decode_exact": 0, "decode_stage": 1}
+              "xcd_min_tiles": 1, "decode_wide_max": 0, "decode_exact": 0, "decode_stage": 1,
+              "image_min_tiles": 1, "image_min_coefs": 0}
     old = {k: codec.get_option(k) for k in values}
     with codec.options(**values):
         assert {k: codec.get_option(k) for k in values} == values
@@ -1033,7 +1034,8 @@ def test_ctx_options_round_trip(codec):
             assert {k: fresh.get_option(k) for k in values} == old
     assert {k: codec.get_option(k) for k in values} == old
     for name, bad in [("rebuild_path", 2), ("rebuild_path", -2), ("pipe_bytes", 1000),
-                      ("decode_exact", 3), ("copy_threads", -1)]:
+                      ("decode_exact", 3), ("copy_threads", -1), ("image_min_tiles", -1),
+                      ("image_min_coefs", -1)]:
         with pytest.raises(ec.MemoECError) as ei:
             codec.set_option(name, bad)
         assert ei.value.code == -1
@@ -1055,8 +1057,20 @@ def test_env_options_keep_their_meanings(monkeypatch, capfd):
         monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", val)
         with ec.Codec(0) as c:
             assert c.get_option("rebuild_path") == want, val
+            assert c.rebuild_path(1, 16, 1 << 30) == ("fused" if want == 1 else "images")
             assert c.rebuild_path(1, 10, 1 << 30) == ("fused" if want == 1 else "rows")
+            assert c.rebuild_path(1 << 20, 16, 4096) == ("fused" if want == 1 else "rows")
     monkeypatch.delenv("MEMO_EC_REBUILD_FUSED")
+    for val, want in [("0", 0), ("1", 1), ("16", 16)]:
+        monkeypatch.setenv("MEMO_EC_IMAGE_MIN_TILES", val)
+        monkeypatch.setenv("MEMO_EC_IMAGE_MIN_COEFS", val)
+        with ec.Codec(0) as c:
+            assert c.get_option("image_min_tiles") == want, val
+            assert c.get_option("image_min_coefs") == want, val
+    monkeypatch.delenv("MEMO_EC_IMAGE_MIN_TILES")
+    monkeypatch.delenv("MEMO_EC_IMAGE_MIN_COEFS")
+    with ec.Codec(0) as c:
+        assert (c.get_option("image_min_tiles"), c.get_option("image_min_coefs")) == (2, 56)
     monkeypatch.setenv("MEMO_EC_COPY_THREADS", "0")
     with ec.Codec(0) as c:
         assert c.get_option("copy_threads") == 1
@@ -1076,8 +1090,16 @@ def test_rebuild_path_label_follows_ctx_options(codec):
     with codec.options(rebuild_path=1):
         assert codec.rebuild_path(1 << 20, 10, 1 << 20) == "fused"
         assert "gf_rebuild_kernel" in codec.rebuild_kernel_name(1 << 20, 10, 1 << 20)
-    with codec.options(rebuild_path=0):
-        assert codec.rebuild_path(1, 10, 64) == "rows"
+    with codec.options(rebuild_path=0, image_min_tiles=2, image_min_coefs=56):
+        assert codec.rebuild_path(1, 16, 64) == "rows"
+        assert codec.rebuild_path(1, 16, 4096) == "rows"          # one tile per block
+        assert codec.rebuild_path(1, 16, 4096 + 64) == "images"   # RS(16,4): 64 coefficients
+        assert codec.rebuild_path(1, 10, 1 << 20) == "rows"       # RS(10,4): 40
+        assert codec.rebuild_path(1, 10, 1 << 20, 6) == "images"  # RS(10,6): 60
+        assert codec.rebuild_path(1, 8, 1 << 20) == "images"      # k = 8: chunk-loop body
+        assert "rows_image_kernel" in codec.rebuild_kernel_name(1, 16, 1 << 20)
+    with codec.options(rebuild_path=0, image_min_tiles=0):
+        assert codec.rebuild_path(1, 16, 1 << 30) == "rows"
 
 
 @pytest.mark.parametrize("kin,r,B,n", [(10, 4, 1 << 20, 64), (16, 4, 4096, 3000), (4, 2, 5000, 33),
