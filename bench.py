@@ -636,9 +636,10 @@ def cpu_baseline(k, m, B, S, seconds, gpu_parity_sample, world=1):
 def c1_case(torch, ec, codec, stream, world=1):
     """BASELINE.json configs[0] (C1): RS(3,2) encode + rebuild (e = 1 and 2
     random erasures per block) of 1000 x 64 KiB blocks.  The CPU oracle
-    (scalar, 16 host threads; the reference-runnable case) is timed beside
+    (scalar, 16 host threads; the reference-runnable case) and the
+    vectorised port (the cpu_baseline's kind, same threads) are timed beside
     the GPU on the same bytes, and every rebuilt shard is compared across
-    the two (whole batch, bit-exact)."""
+    the three (whole batch, bit-exact)."""
     from oracle import oracle as O
     k, m, B, n = 3, 2, 65536, 1000
     S = ec.shard_size(B, k)
@@ -651,22 +652,36 @@ def c1_case(torch, ec, codec, stream, world=1):
     p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
     _, (ek,), _ = timed_steps(torch, [lambda: codec.encode(k, m, d, p)], 20, 20, 0, None, stream)
     ok = bool(np.array_equal(p.cpu().numpy(), par))
+    # the vectorised port (GFNI/AVX-512 or AVX2, the cpu_baseline's kind) on
+    # the same threads and bytes beside the scalar oracle: the fair CPU time
+    simd_par, isa = O.encode_simd(k, m, S, data, threads=threads)
+    t0 = time.perf_counter()
+    O.encode_simd(k, m, S, data, threads=threads, isa=isa, out=simd_par)
+    simd_enc = time.perf_counter() - t0
+    ok = ok and bool(np.array_equal(simd_par, par))
     out = {"workload": "RS(3,2) encode + rebuild (e=1, e=2), 1000 x 65536-byte blocks (BASELINE.json C1)",
            "cpu_threads": threads, "cpu_kind": "port (scalar table oracle)",
-           "encode": {"cpu_ms": round(cpu_enc * 1e3, 3), "gpu_ms": round(float(np.median(ek)), 4)}}
+           "cpu_simd_kind": "port (%s)" % O.SIMD_ISA.get(isa, str(isa)),
+           "encode": {"cpu_ms": round(cpu_enc * 1e3, 3), "cpu_simd_ms": round(simd_enc * 1e3, 3),
+                      "gpu_ms": round(float(np.median(ek)), 4)}}
     for e in (1, 2):
         s_idx, l_idx = O.erasures(SEED, 0, n, k, m, e)
         surv = O.gather(k, m, S, data, par, s_idx)
         t0 = time.perf_counter()
         want = O.rebuild(k, m, S, s_idx, surv, l_idx, threads=threads)
         cpu_reb = time.perf_counter() - t0
+        simd_out, _ = O.rebuild_simd(k, m, S, s_idx, surv, l_idx, threads=threads, isa=isa)
+        t0 = time.perf_counter()
+        O.rebuild_simd(k, m, S, s_idx, surv, l_idx, threads=threads, isa=isa, out=simd_out)
+        simd_reb = time.perf_counter() - t0
+        ok = ok and bool(np.array_equal(simd_out, want))
         sd, ld, sv = (torch.from_numpy(x).cuda() for x in (s_idx, l_idx, surv))
         o = torch.empty((n, e * S), dtype=torch.uint8, device="cuda")
         _, (rk,), _ = timed_steps(torch, [lambda: codec.rebuild(k, m, sd, sv, ld, o)], 20, 20, 0,
                                   None, stream)
         codec.synchronize()
         ok = ok and bool(np.array_equal(o.cpu().numpy(), want))
-        out["rebuild_e%d" % e] = {"cpu_ms": round(cpu_reb * 1e3, 3),
+        out["rebuild_e%d" % e] = {"cpu_ms": round(cpu_reb * 1e3, 3), "cpu_simd_ms": round(simd_reb * 1e3, 3),
                                   "gpu_ms": round(float(np.median(rk)), 4)}
     out["bit_exact"] = ok
     return out
@@ -1064,6 +1079,30 @@ def check_devices(rows, same_device):
             seen[i[key]] = r["rank"]
 
 
+# Legs of the default line that run at N = 1 only (single-GPU workloads, or
+# host-side lines that do not depend on N): named in the N > 1 line itself.
+N1_ONLY_LEGS = [("rebuild_small", "no_small", "1,048,576 x 4 KiB rebuilds: a single-GPU workload"),
+                ("c5_mixed", "no_c5", "BASELINE.json C5 is quoted on 1 GPU"),
+                ("plugin", "no_plugin", "host-side plugin lines, independent of N"),
+                ("sha256", "no_sha", "single-GPU SHA-256 lines"),
+                ("sweep", None, "BASELINE.json C5 sweep is quoted on 1 GPU (--sweep)")]
+
+
+def skipped_at_n(args, world):
+    """{leg: reason} of the legs an N > 1 line leaves out (empty at N = 1);
+    legs the run's flags turned off are not listed."""
+    if world <= 1:
+        return {}
+    out = {}
+    for leg, flag, why in N1_ONLY_LEGS:
+        if flag is None:
+            if getattr(args, "sweep", False):
+                out[leg] = why
+        elif not getattr(args, flag):
+            out[leg] = why
+    return out
+
+
 def assemble(args, world, rows, wall_max, S):
     """The contract line from the ranks' rows (pure: tested on CPU)."""
     from memo_amd.partition import node_report
@@ -1128,6 +1167,8 @@ def assemble(args, world, rows, wall_max, S):
                             "payload / the job's wall time between barriers; pci_bus_id / uuid: "
                             "memo_ec_device_identity of the rank's GPU (distinct ranks on distinct "
                             "GPUs unless --same-device)"}
+    if world > 1:
+        res["skipped_at_n"] = skipped_at_n(args, world)
     return res
 
 
@@ -1217,7 +1258,7 @@ def main():
     if e > 0:
         row["rebuild"] = kstats(kms[1], (k + e) * S * n)
         row["rebuild_bit_exact"] = bool(torch.equal(out, want))
-        row["rebuild_kernel"] = codec.rebuild_kernel_name(n, k, S)
+        row["rebuild_kernel"] = codec.rebuild_kernel_name(n, k, S, e)
         del want
     rows = [row]
     wall_max = wall

@@ -233,8 +233,16 @@ static void *rebuild_thread(void *arg)
     /* the memo pays off over many blocks per thread (the whole-batch checks);
      * a short call (the CPU baseline's sample) decodes every block, as the
      * GPU does, and allocates no cache */
-    const size_t slots = (ek <= 256 && r->b1 - r->b0 >= 1024) ? PAT_CACHE : 1;
+    size_t slots = 1;
+    if (ek <= 256 && r->b1 - r->b0 >= 1024) {
+        /* no more slots than erasure patterns (C(k+m, e)), rounded up to a
+         * power of two: RS(3,2) needs 16, not 8192 entries per thread */
+        double pats = 1.0;
+        for (int i = 0; i < e; ++i) pats = pats * (double)(k + r->m - i) / (double)(i + 1);
+        while (slots < PAT_CACHE && (double)slots < pats) slots <<= 1;
+    }
     uint8_t *cache = (uint8_t *)calloc(slots, ent);
+    if (!cache && slots > 1) cache = (uint8_t *)calloc(slots = 1, ent);  /* no memo, same bytes */
     for (size_t b = r->b0; b < r->b1 && cache; ++b) {
         const uint8_t *sv = r->sidx + b * k, *lv = r->lidx + b * e;
         uint32_t h = 2166136261u;

@@ -170,6 +170,41 @@ def test_bench_assemble_per_rank_fields():
     assert res["host_call_latency"]["encode_4096B_us"] == 20.0
 
 
+def test_bench_assemble_world_8_c4_line():
+    """The first 8-GPU line (C4) is self-describing: eight ranks with
+    distinct device identities give distinct_devices 8, 32768 global blocks
+    (4096 per GPU), and the line names the N = 1-only legs it left out."""
+    import bench
+    args = bench.parse(["--gpus", "8", "--steps", "10"])
+    S = 104896
+    n, B, K = args.blocks, args.block_bytes, 10
+    assert (n, B) == (4096, 1 << 20)
+    rows = [{"rank": r, "device": r, "warmup_steps_run": 40,
+             "device_identity": {"pci_bus_id": "0000:%02x:00.0" % (0x05 + 0x10 * r), "uuid": "%032x" % (0xa0 + r)},
+             "payload_bytes": n * B * 2 * K, "device_seconds": 2.0e-3 * K,
+             "encode": bench.kstats([0.98] * K, 14 * S * n), "rebuild": bench.kstats([1.0] * K, 14 * S * n),
+             "rebuild_bit_exact": True, "rebuild_kernel": "decode + gf_mac_kernel"} for r in range(8)]
+    res = bench.assemble(args, 8, rows, 0.021, S)
+    assert res["n_gpus"] == 8 and res["scaling"] == "weak"
+    assert res["ranks"]["distinct_devices"] == 8
+    assert res["config"]["global_blocks"] == 32768 and res["config"]["blocks_per_gpu"] == 4096
+    assert "C4 at N=8" in res["config"]["workload"]
+    assert len(res["ranks"]["per_gpu"]) == 8
+    assert set(res["skipped_at_n"]) == {"rebuild_small", "c5_mixed", "plugin", "sha256"}
+    assert res["value"] == round(8 * n * B * 2 * K / 0.021 / 2**30, 3)
+    # flags that turn a leg off leave it out of the list; N = 1 lists none
+    quiet = bench.parse(["--gpus", "8", "--no-plugin", "--no-sha", "--sweep"])
+    assert set(bench.skipped_at_n(quiet, 8)) == {"rebuild_small", "c5_mixed", "sweep"}
+    one = bench.parse(["--gpus", "1"])
+    assert bench.skipped_at_n(one, 1) == {}
+    assert "skipped_at_n" not in bench.assemble(one, 1, rows[:1], 0.002, S)
+    # two ranks on one device are refused in an 8-rank line too
+    dup = [dict(r) for r in rows]
+    dup[7]["device_identity"] = dict(dup[3]["device_identity"])
+    with pytest.raises(RuntimeError, match="same GPU"):
+        bench.assemble(args, 8, dup, 0.021, S)
+
+
 def test_cpu_share_is_bounded(monkeypatch):
     """The CPU baseline's threads: at N = 1 the affinity set capped by the
     cgroup quota and OMP_NUM_THREADS; at N > 1 the job's node share (the
@@ -305,6 +340,8 @@ def test_bench_n2_line_is_self_sufficient():
     assert res["roofline"]["traffic"] > 0 and res["roofline"]["traffic_ratio"] < 1.5, res["roofline"]
     assert res["roofline_rebuild"]["traffic"] > 0
     assert res["build_matches_sources"]
+    # the N = 1-only legs it left out are named in the line
+    assert set(res["skipped_at_n"]) == {"c5_mixed", "plugin", "sha256"}
 
 
 def _fake_rocprof(monkeypatch, rows_by_counter):
@@ -429,6 +466,8 @@ def test_bench_default_line_runs_every_leg():
     assert 0 < res["roofline"]["frac_of_achievable"] <= 1.05  # probe timing noise: a few %
     assert res["roofline"]["traffic_ratio"] < 1.1
     assert res["cpu_baseline"]["bit_exact_vs_gpu"] and res["c1"]["bit_exact"]
+    assert res["c1"]["encode"]["cpu_simd_ms"] > 0 and res["c1"]["rebuild_e2"]["cpu_simd_ms"] > 0
+    assert "skipped_at_n" not in res
     assert res["ranks"]["per_gpu"][0]["uuid"] and res["build_matches_sources"]
     for key in ("C2 batch, 1 MiB blocks", "4 KiB blocks"):
         assert res["sha256"][key]["bit_exact"] and res["sha256"][key]["checked"] >= 4096, res["sha256"]

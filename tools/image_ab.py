@@ -5,8 +5,9 @@ body (image_min_tiles 1), beside the encode of the same blocks, per shape.
 The variants alternate in groups of two launches (rotating order), and every
 fifth group's output is compared with the original shards it rebuilds.
 Prints one JSON line per shape: median launch times.
-  usage: image_ab.py [rounds] [launches] [shape ...]   shape = k,m,B (payload ~4 GiB);
-  rounds x launches launches per variant"""
+  usage: image_ab.py [rounds] [launches] [shape ...]   shape = k,m,B[,MiB] (payload,
+  default 4 GiB); rounds x launches launches per variant; AB_FUSED=1 adds the
+  fused gf_rebuild_kernel as a fourth variant"""
 import json
 import os
 import sys
@@ -46,10 +47,12 @@ def main():
         return [a.elapsed_time(b) for a, b in ev]
 
     for shape in shapes:
-        k, m, B = (int(x) for x in shape.split(","))
+        f = [int(x) for x in shape.split(",")]
+        k, m, B = f[:3]
+        mib = f[3] if len(f) > 3 else 4096  # payload per shape
         e = m
         S = ec.shard_size(B, k)
-        n = max(1, (4 << 30) // B)
+        n = max(1, (mib << 20) // B)
         d = torch.empty((n, k * S), dtype=torch.uint8, device="cuda")
         p = torch.empty((n, m * S), dtype=torch.uint8, device="cuda")
         c.fill_blocks(seed, 0, n, B, k, S, d)
@@ -71,15 +74,19 @@ def main():
         # variants alternate in groups of 2 launches, the order rotating per
         # cycle, so clock and power drift fall on every variant alike
         variants = [("encode", None), ("lds", 0), ("images", 1)]
+        if os.environ.get("AB_FUSED"):
+            variants.append(("fused", -1))
         times = {v: [] for v, _ in variants}
-        ok = {"lds": True, "images": True}
+        ok = {"lds": True, "images": True, "fused": True}
         for cyc in range(rounds * launches // 2):
-            rot = cyc % 3
+            rot = cyc % len(variants)
             for name, img in variants[rot:] + variants[:rot]:
                 if img is None:
                     times[name] += timed(lambda: c.encode(k, m, surv, p), 2)
                     continue
-                with c.options(rebuild_path=0, image_min_tiles=img, image_min_coefs=0):
+                opts = dict(rebuild_path=1) if img < 0 else dict(rebuild_path=0, image_min_tiles=img,
+                                                                  image_min_coefs=0)
+                with c.options(**opts):
                     times[name] += timed(lambda: c.rebuild(k, m, sd, surv, ld, out), 2)
                     if cyc % 5 == 0:
                         c.synchronize()
