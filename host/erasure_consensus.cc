@@ -2267,6 +2267,8 @@ struct RegisterErasure {
       o.verify_subsets = get("verify-subsets", o.verify_subsets);
       if (o.batch_max < 1 || stage_mb < 1 || o.threads < 1)
         throw Error("erasure: batch-max, stage-mb and threads must be positive");
+      if (o.fetch_hedge < 0 || o.verify_subsets < 0)
+        throw Error("erasure: fetch-hedge and verify-subsets must not be negative");
       o.stage_bytes = (size_t)stage_mb << 20;
       const int f = get("backend-replication-factor", 3);
       return std::unique_ptr<Consensus>(

@@ -258,6 +258,9 @@ TEST(config_registry, false) {
   CHECK_THROW(make_consensus(ov, "{\"type\": \"nope\"}"), Error);
   CHECK_THROW(make_consensus(ov, "{\"data-shards\": 3}"), Error);
   CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"stage-mb\": 0}"), Error);
+  CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"stage-mb\": -1}"), Error);
+  CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"fetch-hedge\": -1}"), Error);
+  CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"verify-subsets\": -2}"), Error);
   CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"threads\": 0}"), Error);
   auto r = make_consensus(ov, "{\"type\": \"replication\", \"replication-factor\": 2}");
   CHECK(from_json(r->redundancy())["type"] == "replication");

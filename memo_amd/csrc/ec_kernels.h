@@ -101,9 +101,11 @@ struct DecodeArgs {
   uint64_t wide_max;      // batches up to this many blocks: column-per-lane kernel
   uint32_t exact;         // 1: exact-k kernels for k in {2,3,4,6,8,10,12,14,16}
   uint32_t stage;         // 1: exact-k rows staged through LDS
-  // optional: per-block product-table images of the rows (ImageSeg layout,
-  // R x kpad slots per block) -- written by the column-per-lane kernel
-  // itself, by rows_image_kernel behind the other kernels
+  // optional: per-block product-table images of the rows, block b's R x kpad
+  // slots of 8 dwords (table_dword's layout) at img + b * R * kpad * 8, so
+  // gf_mac_kernel runs its encode body over them (tab_bstride = R * kpad * 8);
+  // written by the column-per-lane kernel, which every segment with images
+  // takes (kpad <= its lanes per block)
   uint32_t* img;
   uint32_t R, kpad;
 };
@@ -114,21 +116,6 @@ struct DecodeLaunch {
   uint32_t nseg;
   uint32_t wg_begin[MEMO_EC_MAX_SEGMENTS];
   DecodeArgs seg[MEMO_EC_MAX_SEGMENTS];
-};
-
-// Per-block product-table images formed in HBM from decode rows (the rows
-// path for blocks spanning several tiles): block b's image set, R x kpad
-// slots of 8 dwords (table_dword's layout), at img + b * R * kpad * 8, so
-// gf_mac_kernel runs its encode body with tab_bstride = R * kpad * 8.
-struct ImageSeg {
-  const uint8_t* rows;  // n x e x k decode rows
-  uint32_t* img;        // n x R x kpad x 8 dwords
-  uint32_t n, e, k, R, kpad;
-  uint32_t slot_begin;  // first global slot (thread) of this segment
-};
-struct ImageLaunch {
-  uint32_t nseg;
-  ImageSeg seg[MEMO_EC_MAX_SEGMENTS];
 };
 
 struct Sha256Args {
@@ -165,9 +152,6 @@ hipError_t launch_mac(int KC, int R, int mode, const MacLaunch& L, uint32_t grid
 void lw0_host(int k, int m, uint8_t* out);
 hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st);  // closed-form decode rows
 hipError_t launch_decode_multi(const DecodeArgs* a, int n, hipStream_t st);  // several segments
-// Images of decode rows, several segments per launch; every segment's
-// n * R * kpad slots must fit 31 bits (the caller checks).
-hipError_t launch_images(const ImageSeg* segs, int n, hipStream_t st);
 hipError_t launch_fill(const FillArgs& a, hipStream_t st);
 hipError_t launch_sha256(const Sha256Args& a, hipStream_t st);
 hipError_t launch_gather(const GatherArgs& a, hipStream_t st);

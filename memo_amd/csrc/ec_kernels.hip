@@ -960,14 +960,25 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
   }
 }
 
-// Encode (MAC_ENCODE) and the two-kernel rebuild's MAC (MAC_ROWS).
+// Encode (MAC_ENCODE) and the two-kernel rebuild's MAC (MAC_ROWS).  The
+// rebuild instance also takes segments with table images instead of
+// coefficient rows (coef null: a shared pattern's image, or per-block images
+// the decode formed), so a mixed rebuild's pieces of one shard chunk and row
+// bound share one launch whichever way their tables come (the branch is
+// uniform per workgroup: one segment per tile).
 template <int KC, int R, bool NT, bool COEF>
 __global__ void __launch_bounds__(256) gf_mac_kernel(const MacLaunch L) {
   extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
   uint32_t sid;
   uint64_t tile;
   if (!seg_tile(L, sid, tile)) return;
-  mac_tile<KC, R, NT, COEF ? MAC_ROWS : MAC_ENCODE>(L.seg[sid], tile, s_tab);
+  if constexpr (COEF) {
+    if (L.seg[sid].coef) {
+      mac_tile<KC, R, NT, MAC_ROWS>(L.seg[sid], tile, s_tab);
+      return;
+    }
+  }
+  mac_tile<KC, R, NT, MAC_ENCODE>(L.seg[sid], tile, s_tab);
 }
 
 // Rebuild in one launch: decode rows derived per tile, then the MAC.
@@ -1027,13 +1038,14 @@ __global__ void __launch_bounds__(256) stream_probe_kernel(const MacLaunch L) {
 }
 
 // ---- Per-block product-table images through HBM (rows path, multi-tile
-// blocks).  One lane per slot (block b, row i, column j): the 8-dword image
-// of rows[b][i][j] (zero for the padding rows i >= e and columns j >= k) in
-// table_dword's layout [mid0 mid1 hi0 hi1 lo 0 0 0], two 16-byte stores, so a
-// wave writes 2 KiB contiguous.  The MAC then copies a block's image set like
-// the encode's shared one instead of building it in LDS per tile: for a
-// block of T tiles the build runs once instead of T times, at R * kpad * 32
-// bytes of HBM per block (RS(16,4): 2 KiB, 0.15% of a 1 MiB block's traffic).
+// blocks).  The column-per-lane decode (decode_coef_wide_kernel) writes, for
+// each slot (block b, row i, column j), the 8-dword image of rows[b][i][j]
+// (zero for the padding rows i >= e and columns j >= k) in table_dword's
+// layout [mid0 mid1 hi0 hi1 lo 0 0 0], two 16-byte stores per slot.  The MAC
+// then copies a block's image set like the encode's shared one instead of
+// building it in LDS per tile: for a block of T tiles the build runs once
+// instead of T times, at R * kpad * 32 bytes of HBM per block (RS(16,4):
+// 2 KiB, 0.15% of a 1 MiB block's traffic).
 __device__ __forceinline__ void put_slot_image(uint32_t* img, uint32_t slot, uint32_t c) {
   uint4 q;
   uint32_t lo;
@@ -1041,22 +1053,6 @@ __device__ __forceinline__ void put_slot_image(uint32_t* img, uint32_t slot, uin
   uint4* dst = reinterpret_cast<uint4*>(img + (uint64_t)slot * 8);
   dst[0] = q;
   dst[1] = make_uint4(lo, 0u, 0u, 0u);
-}
-
-__global__ void __launch_bounds__(256) rows_image_kernel(const ImageLaunch L) {
-  const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-  uint32_t sid = 0;
-  for (uint32_t s = 1; s < L.nseg; ++s)
-    if (g >= L.seg[s].slot_begin) sid = s;
-  const ImageSeg& sg = L.seg[sid];
-  const uint32_t per = sg.R * sg.kpad;
-  const uint32_t q = g - sg.slot_begin;
-  if (q >= sg.n * per) return;  // alignment padding between segments
-  const uint32_t b = q / per, rem = q - b * per;
-  const uint32_t i = rem / sg.kpad, j = rem - i * sg.kpad;
-  const uint32_t c =
-      (i < sg.e && j < sg.k) ? sg.rows[(uint64_t)b * sg.e * sg.k + i * sg.k + j] : 0u;
-  put_slot_image(sg.img, q, c);
 }
 
 // ------------------------------------------------- closed-form decode rows
@@ -1904,8 +1900,10 @@ static DecodePick decode_pick(const DecodeArgs& a0) {
   p.a = a0;
   DecodeArgs& a = p.a;
   // Small batches are latency-bound: one lane per survivor column
-  // (a.wide_max: the ctx's MEMO_EC_OPT_DECODE_WIDE_MAX).
-  if (a.n <= a.wide_max) {
+  // (a.wide_max: the ctx's MEMO_EC_OPT_DECODE_WIDE_MAX).  Table images
+  // (a.img) are written by this kernel, lane t the slots of column t, at any
+  // batch size (they go with blocks of several tiles: few blocks per byte).
+  if (a.n <= a.wide_max || a.img) {
     const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
     p.kind = 0;
     p.param = (int)L;
@@ -1985,7 +1983,7 @@ hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
   // of taking a launch of its own (a mixed rebuild's 64 KiB-4 MiB groups
   // beside its 4 KiB group of the same code).
   for (auto& p : picks) {
-    if (p.kind != 0) continue;
+    if (p.kind != 0 || p.a.img) continue;
     DecodeArgs a = p.a;
     a.wide_max = 0;
     const DecodePick r = decode_pick(a);
@@ -1996,20 +1994,8 @@ hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
         break;
       }
   }
-  // Table images: the column-per-lane kernel writes them beside its rows;
-  // behind the other kernels, rows_image_kernel forms them from the rows
-  // (one launch for all such segments, after the decode launches).
-  std::vector<ImageSeg> imgs;
-  for (auto& p : picks) {
-    DecodeArgs& a = p.a;
-    if (!a.img || (p.kind == 0 && a.kpad <= (uint32_t)p.param)) continue;
-    const uint64_t per_dw = (uint64_t)a.R * a.kpad * 8;
-    for (uint64_t b0 = 0; b0 < a.n; b0 += 0x40000000ull)  // ImageSeg.n is 32-bit
-      imgs.push_back({a.rows + b0 * a.e * a.k, a.img + b0 * per_dw,
-                      (uint32_t)std::min<uint64_t>(0x40000000ull, a.n - b0), a.e, a.k, a.R, a.kpad,
-                      0u});
-    a.img = nullptr;
-  }
+  for (const auto& p : picks)  // images: lane t < kpad writes column t's slots
+    if (p.a.img && (p.kind != 0 || p.a.kpad > (uint32_t)p.param)) return hipErrorInvalidValue;
   std::vector<bool> done(picks.size(), false);
   for (size_t i = 0; i < picks.size(); ++i) {
     if (done[i]) continue;
@@ -2029,47 +2015,10 @@ hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
     if (wg > 0x7fffffffull) return hipErrorInvalidValue;
     if (hipError_t e = decode_launch(picks[i].kind, picks[i].param, L, (uint32_t)wg, lds, st)) return e;
   }
-  return imgs.empty() ? hipSuccess : launch_images(imgs.data(), (int)imgs.size(), st);
+  return hipSuccess;
 }
 
 hipError_t launch_decode_coef(const DecodeArgs& a, hipStream_t st) { return launch_decode_multi(&a, 1, st); }
-
-hipError_t launch_images(const ImageSeg* segs, int na, hipStream_t st) {
-  // segments past 2^30 slots are split by blocks, so every launch's slot
-  // numbering fits the kernel's 32-bit arithmetic
-  constexpr uint64_t kMaxSlots = 1ull << 30;
-  std::vector<ImageSeg> parts;
-  for (int i = 0; i < na; ++i) {
-    const ImageSeg& s = segs[i];
-    const uint64_t per = (uint64_t)s.R * s.kpad;
-    if (s.n == 0 || per == 0) continue;
-    if (per > kMaxSlots) return hipErrorInvalidValue;
-    const uint32_t step = (uint32_t)std::min<uint64_t>(s.n, kMaxSlots / per);
-    for (uint32_t b0 = 0; b0 < s.n; b0 += step) {
-      ImageSeg p = s;
-      p.n = std::min(step, s.n - b0);
-      p.rows = s.rows + (uint64_t)b0 * s.e * s.k;
-      p.img = s.img + (uint64_t)b0 * per * 8;
-      parts.push_back(p);
-    }
-  }
-  size_t i = 0;
-  while (i < parts.size()) {
-    ImageLaunch L{};
-    uint64_t slots = 0;
-    for (; i < parts.size() && L.nseg < MEMO_EC_MAX_SEGMENTS; ++i) {
-      const uint64_t cnt = (uint64_t)parts[i].n * parts[i].R * parts[i].kpad;
-      const uint64_t begin = (slots + 255) / 256 * 256;
-      if (L.nseg && begin + cnt > 2 * kMaxSlots) break;  // next launch
-      L.seg[L.nseg] = parts[i];
-      L.seg[L.nseg++].slot_begin = (uint32_t)begin;
-      slots = begin + cnt;
-    }
-    hipLaunchKernelGGL(rows_image_kernel, dim3((uint32_t)((slots + 255) / 256)), dim3(256), 0, st, L);
-    if (hipError_t e = hipGetLastError()) return e;
-  }
-  return hipSuccess;
-}
 
 hipError_t launch_fill(const FillArgs& a, hipStream_t st) {
   const uint64_t total = a.n * (a.stride / 16);

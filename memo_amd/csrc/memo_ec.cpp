@@ -661,7 +661,7 @@ size_t image_bytes(size_t n, int k, int R, int KC) {
 // indices.  Two-kernel: closed-form decode rows (one lane per block) into
 // `scratch` (room for rebuild_scratch(...)), then the MAC, which builds each
 // block's product tables in LDS from its rows, or (rows_images) reads the
-// images rows_image_kernel formed behind the rows.  Faults go to `status`.
+// table images the decode formed beside the rows.  Faults go to `status`.
 int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uint8_t* surv_idx,
                    const uint8_t* surv, const uint8_t* lost_idx, int e, uint8_t* out,
                    bool fused, void* scratch, hipStream_t st, uint32_t* status) {
@@ -1064,14 +1064,25 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
   // every segment's decode rows (and table images), segments of one decode
   // kernel per launch
   if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
+  // The launch class of a piece: (mode, KC, R), where pieces whose tables
+  // come as images (a shared pattern, or per-block images) join the rows
+  // launch of their (KC, R) when the call has one (gf_mac_kernel's rows
+  // instance runs both bodies), so no extra launch tail.
+  auto launch_mode = [&](const RPiece& p) {
+    const int mm = p.mac_mode();
+    if (mm != MAC_ENCODE) return mm;
+    for (const auto& q : ps)
+      if (q.mac_mode() == MAC_ROWS && q.KC == p.KC && q.R == p.R) return (int)MAC_ROWS;
+    return mm;
+  };
   std::vector<bool> done(ps.size(), false);
   for (size_t i = 0; i < ps.size(); ++i) {
     if (done[i]) continue;
-    const int mode = ps[i].mac_mode(), KC = ps[i].KC, R = ps[i].R;
+    const int mode = launch_mode(ps[i]), KC = ps[i].KC, R = ps[i].R;
     std::vector<Plan> plans;
     for (size_t j = i; j < ps.size(); ++j) {
       const auto& p = ps[j];
-      if (done[j] || p.mac_mode() != mode || p.KC != KC || p.R != R) continue;
+      if (done[j] || launch_mode(p) != mode || p.KC != KC || p.R != R) continue;
       done[j] = true;
       const size_t step = max_blocks_per_launch(c, p.S);
       const uint32_t* lw0 = nullptr;
@@ -1082,13 +1093,12 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
         const uint64_t in_bs = (uint64_t)p.k * p.S, out_bs = (uint64_t)p.e * p.S;
         const uint8_t* in = p.surv + b0 * in_bs;
         uint8_t* out = p.out + b0 * out_bs;
-        if (p.img) {
-          const uint64_t per_dw = (uint64_t)R * kpad_of((uint32_t)p.k, KC) * 8;
-          plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
-                                       p.S, pimg[j] + b0 * per_dw, per_dw, KC, R));
-        } else if (mode == MAC_ENCODE) {
-          plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
-                                       p.S, p.tab, 0, KC, R));
+        if (p.img || p.mode == MAC_ENCODE) {
+          const uint64_t per_dw = p.img ? (uint64_t)R * kpad_of((uint32_t)p.k, KC) * 8 : 0;
+          Plan q = plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,
+                                p.S, p.img ? pimg[j] + b0 * per_dw : p.tab, per_dw, KC, R);
+          q.mode = mode;  // encode body; in the rows launch when it joins one
+          plans.push_back(q);
         } else if (mode == MAC_ROWS) {
           const uint64_t row_b = (uint64_t)p.e * p.k;
           plans.push_back(plan_segment((uint32_t)p.k, (uint32_t)p.e, p.S, cnt, in, in_bs, p.S, out, out_bs,

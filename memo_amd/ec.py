@@ -190,9 +190,8 @@ def erasures(seed, first_block, n, k, m, e):
 REBUILD_KERNELS = {"fused": "gf_rebuild_kernel (decode rows per tile + MAC, one launch)",
                    "rows": "decode_coef*/decode_rows_k + gf_mac_kernel (rows through HBM, "
                            "tables built in LDS)",
-                   "images": "decode_coef*/decode_rows_k forming per-block table images "
-                             "(beside the rows, or by rows_image_kernel) + gf_mac_kernel "
-                             "encode body (images through HBM)"}
+                   "images": "decode_coef_wide_kernel forming per-block table images beside "
+                             "the rows + gf_mac_kernel encode body (images through HBM)"}
 
 
 def _is_torch(x):

@@ -40,23 +40,28 @@ def codec():
     c.close()
 
 
-@pytest.fixture(params=["fused", "rows", "images"])
+# rebuild_path param -> (rebuild_path, image_min_tiles, image_min_coefs)
+REBUILD_PATHS = {"fused": (1, 2, 56), "rows": (0, 2, 56), "lds": (0, 0, 56), "images": (0, 1, 0)}
+
+
+@pytest.fixture(params=list(REBUILD_PATHS))
 def rebuild_path(request, monkeypatch):
     """Run a rebuild test on every device rebuild path: the fused
-    gf_rebuild_kernel (default up to 256 MiB), the two-kernel decode rows +
-    gf_mac_kernel path with tables built in LDS ("rows", images off), and
-    the same with per-block table images through HBM for every block size
-    ("images", image_min_tiles 1, image_min_coefs 0): the session codec's
-    options, and MEMO_EC_REBUILD_FUSED / MEMO_EC_IMAGE_MIN_TILES /
-    MEMO_EC_IMAGE_MIN_COEFS for contexts the test creates itself."""
-    v = 1 if request.param == "fused" else 0
-    t = 1 if request.param == "images" else 0
+    gf_rebuild_kernel (default up to 256 MiB); the two-kernel decode rows +
+    gf_mac_kernel path as the defaults choose its tables ("rows": per-block
+    table images through HBM for multi-tile blocks with costly tables,
+    tables built in LDS for the rest, both in one launch of a mixed call);
+    the same with tables always built in LDS ("lds") and with images for
+    every block size ("images"): the session codec's options, and
+    MEMO_EC_REBUILD_FUSED / MEMO_EC_IMAGE_MIN_TILES / MEMO_EC_IMAGE_MIN_COEFS
+    for contexts the test creates itself."""
+    v, t, cf = REBUILD_PATHS[request.param]
     monkeypatch.setenv("MEMO_EC_REBUILD_FUSED", str(v))
     monkeypatch.setenv("MEMO_EC_IMAGE_MIN_TILES", str(t))
-    monkeypatch.setenv("MEMO_EC_IMAGE_MIN_COEFS", "0")
+    monkeypatch.setenv("MEMO_EC_IMAGE_MIN_COEFS", str(cf))
     if "codec" in request.fixturenames:
         c = request.getfixturevalue("codec")
-        with c.options(rebuild_path=v, image_min_tiles=t, image_min_coefs=0):
+        with c.options(rebuild_path=v, image_min_tiles=t, image_min_coefs=cf):
             yield request.param
     else:
         yield request.param

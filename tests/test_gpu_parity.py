@@ -1097,7 +1097,7 @@ def test_rebuild_path_label_follows_ctx_options(codec):
         assert codec.rebuild_path(1, 10, 1 << 20) == "rows"       # RS(10,4): 40
         assert codec.rebuild_path(1, 10, 1 << 20, 6) == "images"  # RS(10,6): 60
         assert codec.rebuild_path(1, 8, 1 << 20) == "images"      # k = 8: chunk-loop body
-        assert "rows_image_kernel" in codec.rebuild_kernel_name(1, 16, 1 << 20)
+        assert "table images" in codec.rebuild_kernel_name(1, 16, 1 << 20)
     with codec.options(rebuild_path=0, image_min_tiles=0):
         assert codec.rebuild_path(1, 16, 1 << 30) == "rows"
 
