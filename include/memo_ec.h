@@ -142,13 +142,14 @@ enum memo_ec_option {
                                            through LDS (0)                       */
     MEMO_EC_OPT_IMAGE_MIN_TILES = 11,   /* MEMO_EC_IMAGE_MIN_TILES: the decode rows +
                                            MAC rebuild forms per-block product-
-                                           table images in HBM for blocks of at
-                                           least this many 4 KiB shard tiles and
-                                           runs the encode body over them
-                                           (2; 0: never, tables built in LDS)    */
+                                           table images in HBM for shards of at
+                                           least this many whole 4 KiB tiles
+                                           (S / 4096) and runs the encode body
+                                           over them (1; 0: never, tables built
+                                           in LDS)                               */
     MEMO_EC_OPT_IMAGE_MIN_COEFS = 12    /* MEMO_EC_IMAGE_MIN_COEFS: ... and at least
                                            this many coefficients per block
-                                           (padded rows x columns; 56) or a k
+                                           (padded rows x columns; 40) or a k
                                            without a straight-line MAC body      */
 };
 

@@ -20,8 +20,10 @@ namespace memo_ec {
 //    rebuild's LDS cycles in bank conflicts);
 //  - straight-line bodies for k = 6, 12, 14 (R <= 4) besides 2, 3, 4, 10, 16.
 constexpr bool MAC_NT = true;
-// Table dwords per lane staged through registers ahead of the shard loads.
-constexpr int MAC_TAB_REGS = 2;
+// Table dwords per lane staged through registers ahead of the shard loads:
+// two sets of R x kpad <= 64 images (a tile across two blocks' per-block
+// images); the encode's one shared set needs two.
+constexpr int MAC_TAB_REGS = 4;
 // Coefficients per lane staged through registers (rebuild tables built in
 // LDS): 256 * 6 = 1536 slots, the most a flat-mapped rebuild tile builds
 // (launch planning in memo_ec.cpp keeps to it).

@@ -1519,11 +1519,13 @@ __global__ void __launch_bounds__(256) decode_rows_k_kernel(const DecodeLaunch D
 
 // Latency variant for small batches: L lanes per block (L = the power of two
 // >= k), lane t owns survivor column t.  The block's survivor bit set is
-// OR-reduced across its L lanes; each lane then needs only its own W_t
-// (m lookups) and, per lost shard, Lam_l (m lookups) and one coefficient.
-// About k + m + e * (k + m + 2) lookups per lane against the per-block
-// kernel's k * m + e * (m + 2k) in one lane: a few microseconds for a
-// C3-sized batch instead of ~15.
+// OR-reduced across its L lanes and its m non-survivors c are extracted into
+// registers (as in the exact-k kernel); each lane then needs only its own
+// W_t (m lookups) and, per lost shard, Lam_l (m lookups) and one
+// coefficient: about (e + 1) * (m + 1) + e lookups per lane.  A C3-sized
+// batch takes a few microseconds.  (Round 1-4 looped every lane over all
+// k + m indices with a survivor mask, 3-4x the lookups: 36 us for 65,536
+// RS(16,4) blocks, profiles/r05_decode_probe.jsonl.)
 template <int L>
 __global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunch DL) {
   uint32_t bid;
@@ -1532,7 +1534,7 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunc
   __shared__ uint32_t s_lw0[MEMO_EC_MAX_K + MEMO_EC_MAX_M];
   const uint8_t* lg = reinterpret_cast<const uint8_t*>(s_gf);
   const uint8_t* ex = lg + 256;
-  const uint32_t k = a.k, e = a.e, nt = a.k + a.m, ek = a.e * a.k;
+  const uint32_t k = a.k, m = a.m, e = a.e, nt = a.k + a.m, ek = a.e * a.k;
   const uint32_t t = threadIdx.x % L;
   const uint64_t b = (uint64_t)bid * (256 / L) + threadIdx.x / L;
   const bool live = b < a.n;  // whole groups
@@ -1548,9 +1550,13 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunc
     lv[q] = (live && r < e) ? a.lost_idx[b * e + r] : 0u;
   }
   stage_gf(s_gf);
+  if (a.lw0)  // LW0 of (k, m) from the host (lw0_host), one byte per index
+    for (uint32_t i = threadIdx.x; i < nt; i += 256) s_lw0[i] = reinterpret_cast<const uint8_t*>(a.lw0)[i];
   __syncthreads();
-  stage_lw0(lg, k, nt, s_lw0);
-  __syncthreads();
+  if (!a.lw0) {
+    stage_lw0(lg, k, nt, s_lw0);
+    __syncthreads();
+  }
   if (!live) return;  // no barrier below
   bool bad = col && sv >= nt;
   uint32_t mk[3] = {0u, 0u, 0u};
@@ -1574,14 +1580,36 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunc
     const uint32_t w = v >> 5, bit = 1u << (v & 31);
     return ((w == 0 ? mk[0] : (w == 1 ? mk[1] : mk[2])) & bit) != 0;
   };
-  uint32_t lw = 0;  // log W_t
+  // the m non-survivors (indices < nt outside the survivor set), in
+  // registers; a faulty set may run out (its rows are zero anyway)
+  uint32_t cl[MEMO_EC_MAX_M];
+  {
+    uint32_t c0 = ~mk[0] & (nt >= 32 ? ~0u : (1u << nt) - 1u);
+    uint32_t c1 = nt <= 32 ? 0u : ~mk[1] & (nt >= 64 ? ~0u : (1u << (nt - 32)) - 1u);
+    uint32_t c2 = nt <= 64 ? 0u : ~mk[2] & ((1u << (nt - 64)) - 1u);
+#pragma unroll
+    for (int q = 0; q < MEMO_EC_MAX_M; ++q) {
+      cl[q] = 0u;
+      if ((uint32_t)q < m) {
+        if (c0) {
+          cl[q] = __builtin_ctz(c0);
+          c0 &= c0 - 1;
+        } else if (c1) {
+          cl[q] = 32u + __builtin_ctz(c1);
+          c1 &= c1 - 1;
+        } else if (c2) {
+          cl[q] = 64u + __builtin_ctz(c2);
+          c2 &= c2 - 1;
+        }
+      }
+    }
+  }
+  uint32_t lw = 0;  // log W_t = LW0(s_t) + sum_c log(s_t ^ c)
   if (col && !bad) {
     lw = s_lw0[sv];
-#pragma unroll 8
-    for (uint32_t i = 0; i < nt; ++i) {
-      const uint32_t v = lg[sv ^ i];
-      lw += is_surv(i) ? 0u : v;
-    }
+#pragma unroll
+    for (int q = 0; q < MEMO_EC_MAX_M; ++q)
+      if ((uint32_t)q < m) lw += lg[sv ^ cl[q]];
     lw = mod255(lw);
   }
   uint8_t* out = a.rows + b * (uint64_t)ek;
@@ -1594,14 +1622,12 @@ __global__ void __launch_bounds__(256) decode_coef_wide_kernel(const DecodeLaunc
     const uint32_t l = __shfl(mine, r % L, L);  // the same for the whole group
     bad |= l >= nt;
     const bool unit = !bad && is_surv(l);
-    uint32_t llam = 0;  // log Lam_l
+    uint32_t llam = 0;  // log Lam_l = -(LW0(l) + sum_{c != l} log(l ^ c))
     if (!bad && !unit) {
-      uint32_t acc = s_lw0[l];  // i == l adds log[0] = 0
-#pragma unroll 8
-      for (uint32_t i = 0; i < nt; ++i) {
-        const uint32_t v = lg[l ^ i];
-        acc += is_surv(i) ? 0u : v;
-      }
+      uint32_t acc = s_lw0[l];  // c == l adds log[0] = 0
+#pragma unroll
+      for (int q = 0; q < MEMO_EC_MAX_M; ++q)
+        if ((uint32_t)q < m) acc += lg[l ^ cl[q]];
       llam = 255u - mod255(acc);
     }
     uint32_t v = 0;
@@ -1899,40 +1925,47 @@ static DecodePick decode_pick(const DecodeArgs& a0) {
   DecodePick p;
   p.a = a0;
   DecodeArgs& a = p.a;
-  // Small batches are latency-bound: one lane per survivor column
-  // (a.wide_max: the ctx's MEMO_EC_OPT_DECODE_WIDE_MAX).  Table images
-  // (a.img) are written by this kernel, lane t the slots of column t, at any
-  // batch size (they go with blocks of several tiles: few blocks per byte).
-  if (a.n <= a.wide_max || a.img) {
-    const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
-    p.kind = 0;
-    p.param = (int)L;
-    p.grid = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
-    return p;
-  }
-  p.grid = (uint32_t)((a.n + 255) / 256);
   // LDS staging of the rows: pitch = e*k rounded up to an odd dword count
   const uint32_t ek = a.e * a.k;
   uint32_t pw = (ek + 3) / 4;
   pw |= 1u;
   a.pitch = 256u * pw * 4 <= 64 * 1024 ? pw * 4 : 0u;
   const size_t lds = a.pitch ? 256u * a.pitch : 0;
-  // exact-k kernels for the common codes, k in {2, 3, 4, 6, 8, 10, 12, 14,
-  // 16} (a.exact), storing whole-dword rows straight from registers unless
-  // a.stage asks for the LDS staging (A/B runs and tests)
+  // 1. the exact-k kernels for the common codes, k in {2, 3, 4, 6, 8, 10,
+  // 12, 14, 16} (a.exact), storing whole-dword rows straight from registers
+  // unless a.stage asks for the LDS staging (A/B runs and tests): one lane
+  // per block is the fastest form at every batch size, 256 blocks to
+  // 64 Ki (6.3-7.9 us, against 7.8-17.7 for the column-per-lane kernel;
+  // profiles/r05_decode_probe.jsonl).  Not for table images (below).
   DecodeArgs ax = a;
   if (!a.stage && (ek & 3) == 0 && (reinterpret_cast<uintptr_t>(a.rows) & 3) == 0) ax.pitch = 0;
   const bool exact_k = a.k == 2 || a.k == 3 || a.k == 4 || a.k == 6 || a.k == 8 || a.k == 10 ||
                        a.k == 12 || a.k == 14 || a.k == 16;
-  if (a.exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32 && exact_k) {
+  if (!a.img && a.exact && (a.pitch || !ax.pitch) && a.lw0 && a.k + a.m <= 32 && exact_k) {
     p.kind = 1;
     p.param = (int)a.k + (a.m <= 4 ? 0 : 100);  // m bound 4 or MEMO_EC_MAX_M
+    p.grid = (uint32_t)((a.n + 255) / 256);
     p.lds = ax.pitch ? lds : 0;
     p.a = ax;
     return p;
   }
+  // 2. the column-per-lane kernel: other k up to a.wide_max blocks (the
+  // ctx's MEMO_EC_OPT_DECODE_WIDE_MAX; the generic one-lane kernel takes
+  // 1.6-4x longer there), and any batch whose table images it writes beside
+  // the rows, lane t the slots of column t (images go with blocks of whole
+  // tiles: few blocks per byte)
+  if (a.n <= a.wide_max || a.img) {
+    const uint32_t L = a.k <= 4 ? 4 : a.k <= 8 ? 8 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
+    p.kind = 0;
+    p.param = (int)L;
+    p.grid = (uint32_t)((a.n + 256 / L - 1) / (256 / L));
+    p.a.pitch = 0;
+    return p;
+  }
+  // 3. the generic one-lane-per-block kernel
   p.kind = 2;
   p.param = a.k <= 4 ? 4 : a.k <= 10 ? 10 : a.k <= 16 ? 16 : a.k <= 32 ? 32 : 64;
+  p.grid = (uint32_t)((a.n + 255) / 256);
   p.lds = lds;
   return p;
 }
@@ -1978,22 +2011,6 @@ hipError_t launch_decode_multi(const DecodeArgs* as, int na, hipStream_t st) {
   std::vector<DecodePick> picks;
   for (int i = 0; i < na; ++i)
     if (as[i].n) picks.push_back(decode_pick(as[i]));
-  // A segment small enough for the column-per-lane kernel rides in the
-  // exact-k launch of another segment with the same k and m bound, instead
-  // of taking a launch of its own (a mixed rebuild's 64 KiB-4 MiB groups
-  // beside its 4 KiB group of the same code).
-  for (auto& p : picks) {
-    if (p.kind != 0 || p.a.img) continue;
-    DecodeArgs a = p.a;
-    a.wide_max = 0;
-    const DecodePick r = decode_pick(a);
-    if (r.kind != 1) continue;
-    for (const auto& q : picks)
-      if (q.kind == 1 && q.param == r.param) {
-        p = r;
-        break;
-      }
-  }
   for (const auto& p : picks)  // images: lane t < kpad writes column t's slots
     if (p.a.img && (p.kind != 0 || p.a.kpad > (uint32_t)p.param)) return hipErrorInvalidValue;
   std::vector<bool> done(picks.size(), false);

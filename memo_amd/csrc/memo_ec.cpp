@@ -36,8 +36,8 @@ struct memo_ec_opts {
   uint64_t decode_wide_max = 65536;       // column-per-lane decode up to this many blocks
   int decode_exact = 1;
   int decode_stage = 0;
-  uint64_t image_min_tiles = 2;           // rows path: HBM table images from this many tiles/block
-  uint64_t image_min_coefs = 56;          //   and this many coefficients per block (R x kpad)
+  uint64_t image_min_tiles = 1;           // rows path: HBM table images from this many whole tiles
+  uint64_t image_min_coefs = 40;          //   per shard and this many coefficients (R x kpad)
 };
 
 struct memo_ec_ctx {
@@ -288,6 +288,12 @@ Plan plan_segment(uint32_t kin, uint32_t r, size_t S, size_t n, const uint8_t* i
   uint64_t sets;
   if (per_coef ? coef_bs == 0 : tab_bs_dw == 0) {  // one table set for every block
     s.flat = 1;
+    sets = 1;
+  } else if (!per_coef && C >= MAC_TILE && sets_per_tile(C) * per * 8 > 256u * MAC_TAB_REGS) {
+    // per-block table images too large for a tile across two blocks to stage
+    // both sets in registers ahead of its shard loads (R x kpad > 64): tiles
+    // inside one block
+    s.flat = 0;
     sets = 1;
   } else if (sets_per_tile(C) * set_bytes <= kLdsBudget &&
              (!per_coef || sets_per_tile(C) * per <= 256u * MAC_COEF_REGS)) {
@@ -641,7 +647,7 @@ DecodeArgs decode_args(const memo_ec_ctx* c, int k, int m, int e, size_t n, cons
 // one-tile blocks -0.1 (RS(16,4) 64 KiB) to -60 (4 KiB).
 bool rows_images(const memo_ec_ctx* c, size_t S, int k, int R, int KC) {
   const uint64_t t = c->opt.image_min_tiles;
-  if (t == 0 || (S / 16 + MAC_TILE - 1) / MAC_TILE < t) return false;
+  if (t == 0 || S / 16 / MAC_TILE < t) return false;  // whole tiles per shard
   return KC != k || (uint64_t)R * kpad_of((uint32_t)k, KC) >= c->opt.image_min_coefs;
 }
 size_t round256(size_t b) { return (b + 255) & ~(size_t)255; }

@@ -304,11 +304,11 @@ class Codec:
 
     def uses_images(self, k, S, e=None):
         """Whether the rows path forms per-block table images in HBM for
-        this geometry (memo_ec.cpp rows_images): blocks of >= image_min_tiles
-        4 KiB shard tiles whose R x kpad coefficients reach image_min_coefs,
+        this geometry (memo_ec.cpp rows_images): shards of >= image_min_tiles
+        whole 4 KiB tiles whose R x kpad coefficients reach image_min_coefs,
         or any k without a straight-line MAC body.  e defaults to 4."""
         t = self.get_option("image_min_tiles")
-        if not t or -(-S // 4096) < t:
+        if not t or S // 4096 < t:
             return False
         R = mac_rbound(4 if e is None else e)
         KC = mac_kchunk(k, R)

@@ -41,7 +41,7 @@ def codec():
 
 
 # rebuild_path param -> (rebuild_path, image_min_tiles, image_min_coefs)
-REBUILD_PATHS = {"fused": (1, 2, 56), "rows": (0, 2, 56), "lds": (0, 0, 56), "images": (0, 1, 0)}
+REBUILD_PATHS = {"fused": (1, 1, 40), "rows": (0, 1, 40), "lds": (0, 0, 40), "images": (0, 1, 0)}
 
 
 @pytest.fixture(params=list(REBUILD_PATHS))

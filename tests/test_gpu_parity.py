@@ -227,16 +227,16 @@ def test_decode_rows_vs_oracle(codec, O, k, m, kernel):
     C[lost] * inv(C[surv]): random survivor orders, lost shards that are
     data, parity or themselves survivors (unit rows), e = 1..m, over 700
     blocks (several workgroups).  Both kernels: column-per-lane
-    (decode_coef_wide_kernel, small batches) and one lane per block
-    (forced by decode_wide_max=0: decode_rows_k_kernel for k in
-    {2, 3, 4, 6, 8, 10, 12, 14, 16}, decode_coef_kernel otherwise or with
-    decode_exact=0).  The exact-k kernel stores whole-dword rows from
+    (decode_coef_wide_kernel: forced by decode_exact=0 for every k) and
+    one lane per block (decode_rows_k_kernel for k in {2, 3, 4, 6, 8, 10,
+    12, 14, 16}, decode_coef_kernel otherwise -- forced by decode_wide_max=0
+    -- or with decode_exact=0).  The exact-k kernel stores whole-dword rows from
     registers, other rows through LDS (all of them with decode_stage=1)."""
     with codec.options(**DECODE_KERNELS[kernel]):
         _decode_rows_vs_oracle(codec, O, k, m)
 
 
-DECODE_KERNELS = {"wide": {}, "per_block": {"decode_wide_max": 0},
+DECODE_KERNELS = {"wide": {"decode_exact": 0, "decode_wide_max": 1 << 20}, "per_block": {"decode_wide_max": 0},
                   "per_block_staged": {"decode_wide_max": 0, "decode_stage": 1},
                   "per_block_generic": {"decode_wide_max": 0, "decode_exact": 0}}
 
@@ -1058,8 +1058,8 @@ def test_env_options_keep_their_meanings(monkeypatch, capfd):
         with ec.Codec(0) as c:
             assert c.get_option("rebuild_path") == want, val
             assert c.rebuild_path(1, 16, 1 << 30) == ("fused" if want == 1 else "images")
-            assert c.rebuild_path(1, 10, 1 << 30) == ("fused" if want == 1 else "rows")
-            assert c.rebuild_path(1 << 20, 16, 4096) == ("fused" if want == 1 else "rows")
+            assert c.rebuild_path(1, 4, 1 << 30, 2) == ("fused" if want == 1 else "rows")
+            assert c.rebuild_path(1 << 20, 16, 256) == ("fused" if want == 1 else "rows")
     monkeypatch.delenv("MEMO_EC_REBUILD_FUSED")
     for val, want in [("0", 0), ("1", 1), ("16", 16)]:
         monkeypatch.setenv("MEMO_EC_IMAGE_MIN_TILES", val)
@@ -1070,7 +1070,7 @@ def test_env_options_keep_their_meanings(monkeypatch, capfd):
     monkeypatch.delenv("MEMO_EC_IMAGE_MIN_TILES")
     monkeypatch.delenv("MEMO_EC_IMAGE_MIN_COEFS")
     with ec.Codec(0) as c:
-        assert (c.get_option("image_min_tiles"), c.get_option("image_min_coefs")) == (2, 56)
+        assert (c.get_option("image_min_tiles"), c.get_option("image_min_coefs")) == (1, 40)
     monkeypatch.setenv("MEMO_EC_COPY_THREADS", "0")
     with ec.Codec(0) as c:
         assert c.get_option("copy_threads") == 1
@@ -1086,16 +1086,17 @@ def test_rebuild_path_label_follows_ctx_options(codec):
     rebuild kernel with it), not the environment."""
     with codec.options(rebuild_path=-1, fused_max_bytes=1 << 20):
         assert codec.rebuild_path(16, 10, 4096) == "fused"
-        assert codec.rebuild_path(1024, 10, 4096) == "rows"
+        assert codec.rebuild_path(1024, 10, 2048) == "rows"
     with codec.options(rebuild_path=1):
         assert codec.rebuild_path(1 << 20, 10, 1 << 20) == "fused"
         assert "gf_rebuild_kernel" in codec.rebuild_kernel_name(1 << 20, 10, 1 << 20)
-    with codec.options(rebuild_path=0, image_min_tiles=2, image_min_coefs=56):
+    with codec.options(rebuild_path=0, image_min_tiles=1, image_min_coefs=40):
         assert codec.rebuild_path(1, 16, 64) == "rows"
-        assert codec.rebuild_path(1, 16, 4096) == "rows"          # one tile per block
-        assert codec.rebuild_path(1, 16, 4096 + 64) == "images"   # RS(16,4): 64 coefficients
-        assert codec.rebuild_path(1, 10, 1 << 20) == "rows"       # RS(10,4): 40
-        assert codec.rebuild_path(1, 10, 1 << 20, 6) == "images"  # RS(10,6): 60
+        assert codec.rebuild_path(1, 16, 4096 - 64) == "rows"     # less than one whole tile
+        assert codec.rebuild_path(1, 16, 4096) == "images"        # RS(16,4): 64 coefficients
+        assert codec.rebuild_path(1, 10, 1 << 20) == "images"     # RS(10,4): 40
+        assert codec.rebuild_path(1, 6, 1 << 20, 3) == "rows"     # RS(6,3): 18
+        assert codec.rebuild_path(1, 4, 1 << 20, 2) == "rows"     # RS(4,2): 8
         assert codec.rebuild_path(1, 8, 1 << 20) == "images"      # k = 8: chunk-loop body
         assert "table images" in codec.rebuild_kernel_name(1, 16, 1 << 20)
     with codec.options(rebuild_path=0, image_min_tiles=0):

@@ -1,6 +1,7 @@
 #!/bin/bash
 # One GPU iteration call: the GPU tests (SEL selects with -k; empty: all),
-# smoke, then optional probes named in PROBES ("image_ab", "bench", "host").
+# smoke, then optional probes named in PROBES ("image_ab", "host", "bench",
+# "sweep", "profile": tools/profile.sh, "pmc4k": tools/pmc_4k.sh).
 # Every GPU step has its own time limit; the first failure ends the call.
 set -e
 TAG=${1:-iter}
@@ -18,6 +19,8 @@ for p in $PROBES; do
     host) timeout -k 10 300 host/_build/test_erasure > $OUT/host_tests.log 2>&1 ;;
     bench) timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench.json 2> $OUT/bench.err ;;
     sweep) timeout -k 10 900 python bench.py --sweep --no-pmc --no-plugin --no-sha > $OUT/sweep.json 2> $OUT/sweep.err ;;
+    profile) OUT=$OUT/prof bash tools/profile.sh > $OUT/profile.log 2>&1 ;;
+    pmc4k) OUT=$OUT/pmc_4k bash tools/pmc_4k.sh > $OUT/pmc_4k.log 2>&1 ;;
   esac
 done
 echo done
