@@ -823,6 +823,8 @@ def pmc_traffic(args, result, local, world):
              "--erasures", str(e)]
 
     def kind(name):
+        if "gf_mac_images_kernel" in name:  # the rebuild MAC over per-block table images
+            return "rebuild"
         if "gf_mac_kernel" in name:
             return "rebuild" if name.split("(")[0].rstrip(">").rstrip().endswith("true") else "encode"
         if "gf_rebuild_kernel" in name or "decode_" in name:

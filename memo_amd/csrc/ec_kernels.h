@@ -38,7 +38,10 @@ constexpr int DEC_IDX_REGS = 2;
 // per-block coefficient row from decode_coef_kernel (two-kernel rebuild), or
 // rows the tile derives from the shard indices itself (fused rebuild).
 // MAC_PROBE: the same traffic without the GF arithmetic (stream_probe_kernel).
-enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2, MAC_PROBE = 3 };
+// MAC_IMAGES: a rebuild over per-block table images -- the encode's code
+// under a kernel name of its own (gf_mac_images_kernel), so traces tell a
+// rebuild MAC from an encode.
+enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2, MAC_PROBE = 3, MAC_IMAGES = 4 };
 
 // LDS bytes of the fused rebuild's decode workspace for a tile of ns blocks:
 // GF log/antilog (1 KiB), LW0 (128 B), per block 3 survivor-mask words + a

@@ -981,6 +981,17 @@ __global__ void __launch_bounds__(256) gf_mac_kernel(const MacLaunch L) {
   mac_tile<KC, R, NT, MAC_ENCODE>(L.seg[sid], tile, s_tab);
 }
 
+// The two-kernel rebuild's MAC over per-block table images (the decode
+// formed them in HBM): gf_mac_kernel's encode instance under its own name.
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256) gf_mac_images_kernel(const MacLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
+  uint32_t sid;
+  uint64_t tile;
+  if (!seg_tile(L, sid, tile)) return;
+  mac_tile<KC, R, NT, MAC_ENCODE>(L.seg[sid], tile, s_tab);
+}
+
 // Rebuild in one launch: decode rows derived per tile, then the MAC.
 template <int KC, int R, bool NT>
 __global__ void __launch_bounds__(256) gf_rebuild_kernel(const MacLaunch L) {
@@ -1848,6 +1859,8 @@ static hipError_t launch_mac_t(int mode, const MacLaunch& L, uint32_t grid, size
     hipLaunchKernelGGL((gf_rebuild_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
   else if (mode == MAC_ROWS)
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, true>), dim3(grid), dim3(256), lds, st, L);
+  else if (mode == MAC_IMAGES)
+    hipLaunchKernelGGL((gf_mac_images_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
   else
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, false>), dim3(grid), dim3(256), lds, st, L);
   return hipGetLastError();

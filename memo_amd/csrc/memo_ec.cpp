@@ -710,6 +710,7 @@ int rebuild_device(memo_ec_ctx* ctx, int k, int m, size_t S, size_t n, const uin
                : plan_segment((uint32_t)k, (uint32_t)e, S, cnt, surv + b0 * (size_t)k * S,
                               (uint64_t)k * S, S, out + b0 * (size_t)e * S, (uint64_t)e * S, S,
                               nullptr, 0, KC, R, rows + b0 * row_b, row_b, (uint32_t)e)};
+    if (images) plans[0].mode = MAC_IMAGES;  // the encode's code under a rebuild name
     if (int rc = launch_plans(ctx, plans, st)) return rc;
   }
   return MEMO_EC_OK;
@@ -1070,16 +1071,23 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
   // every segment's decode rows (and table images), segments of one decode
   // kernel per launch
   if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
-  // The launch class of a piece: (mode, KC, R), where pieces whose tables
-  // come as images (a shared pattern, or per-block images) join the rows
-  // launch of their (KC, R) when the call has one (gf_mac_kernel's rows
-  // instance runs both bodies), so no extra launch tail.
-  auto launch_mode = [&](const RPiece& p) {
-    const int mm = p.mac_mode();
-    if (mm != MAC_ENCODE) return mm;
+  // The launch class of a piece: (mode, KC, R).  Pieces that multiply with
+  // table images -- per-block images, or a shared pattern's -- join the
+  // rows launch of their (KC, R) when the call has one (gf_mac_kernel's
+  // rows instance runs both bodies: no extra launch tail); otherwise
+  // per-block images take gf_mac_images_kernel (the encode's code under a
+  // rebuild name: kernel traces tell it from the encode), and a shared
+  // pattern joins that launch, or the encode kernel.
+  auto has = [&](const RPiece& p, bool images) {
     for (const auto& q : ps)
-      if (q.mac_mode() == MAC_ROWS && q.KC == p.KC && q.R == p.R) return (int)MAC_ROWS;
-    return mm;
+      if (q.KC == p.KC && q.R == p.R && (images ? q.img : q.mac_mode() == MAC_ROWS)) return true;
+    return false;
+  };
+  auto launch_mode = [&](const RPiece& p) {
+    if (p.mac_mode() != MAC_ENCODE) return p.mac_mode();  // rows, fused
+    if (has(p, false)) return (int)MAC_ROWS;
+    if (p.img || has(p, true)) return (int)MAC_IMAGES;
+    return (int)MAC_ENCODE;
   };
   std::vector<bool> done(ps.size(), false);
   for (size_t i = 0; i < ps.size(); ++i) {

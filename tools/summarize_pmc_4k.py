@@ -24,6 +24,8 @@ SIMDS = 256 * 4
 def short(name):
     if "gf_rebuild_kernel" in name:
         return "gf_rebuild_kernel (fused)"
+    if "gf_mac_images_kernel" in name:
+        return "rebuild MAC"
     if "gf_mac_kernel" in name:
         return "rebuild MAC" if name.rstrip(")").split("(")[0].endswith("true>") else "encode MAC"
     if "decode_" in name:

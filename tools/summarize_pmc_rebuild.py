@@ -16,6 +16,8 @@ base = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_rebuild"
 def short(name):
     if "gf_rebuild_kernel" in name:
         return "gf_rebuild_kernel (fused)"
+    if "gf_mac_images_kernel" in name:
+        return "gf_mac_images_kernel rebuild MAC"
     if "gf_mac_kernel" in name:
         return "gf_mac_kernel rebuild MAC" if name.rstrip(")").split("(")[0].endswith("true>") \
             else "gf_mac_kernel encode"

@@ -8,8 +8,9 @@ Writes
 (bench.py measures roofline.traffic itself, with its own counter passes.)
 
 The encode (gf_mac_kernel<KC, R, NT, false>) and the rebuild MAC
-(gf_mac_kernel<..., true>, after decode_coef*/decode_rows_k*) are told apart
-by their template arguments.  HBM bytes per launch = (2 * FETCH_SIZE +
+(gf_mac_images_kernel<KC, R, NT> over per-block table images, or
+gf_mac_kernel<..., true> with tables built in LDS; after the decode-rows
+kernel) are told apart by their names.  HBM bytes per launch = (2 * FETCH_SIZE +
 WRITE_SIZE) * 1024: on gfx950 FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read and WRITE_SIZE is exact for 16-byte-per-lane stores
 (MI355X_MICROARCH.md, HBM).
@@ -30,6 +31,8 @@ def rows(path):
 
 
 def kind(name):
+    if "gf_mac_images_kernel" in name:
+        return "rebuild_mac"
     if name.startswith("void memo_ec::gf_mac_kernel") or name.startswith("memo_ec::gf_mac_kernel"):
         return "rebuild_mac" if name.split("(")[0].rstrip(">").rstrip().endswith("true") else "encode"
     if "gf_rebuild_kernel" in name:
@@ -84,7 +87,8 @@ def main():
     md.append("")
     for kd, label, key in (("encode", "encode MAC (gf_mac_kernel<10, 4, true, false>)",
                             "encode_%d_%d_%d_%d" % (k, m, B, n)),
-                           ("rebuild_mac", "rebuild MAC (gf_mac_kernel<10, 4, true, true>)",
+                           ("rebuild_mac", "rebuild MAC (gf_mac_images_kernel<10, 4, true>, or "
+                            "gf_mac_kernel<10, 4, true, true> with tables built in LDS)",
                             "rebuild_%d_%d_%d_%d_e%d" % (k, m, B, n, e))):
         d = durs.get(kd, [])
         if not d:
