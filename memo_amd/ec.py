@@ -307,7 +307,10 @@ class Codec:
         this geometry (memo_ec.cpp rows_images): shards of >= image_min_tiles
         whole 4 KiB tiles whose R x kpad coefficients reach image_min_coefs,
         or any k without a straight-line MAC body.  e defaults to 4."""
-        t = self.get_option("image_min_tiles")
+        try:
+            t = self.get_option("image_min_tiles")
+        except MemoECError:  # a library from before the option (A/B runs of older builds)
+            return False
         if not t or S // 4096 < t:
             return False
         R = mac_rbound(4 if e is None else e)
