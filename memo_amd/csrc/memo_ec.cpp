@@ -633,18 +633,19 @@ DecodeArgs decode_args(const memo_ec_ctx* c, int k, int m, int e, size_t n, cons
 }
 
 // Rows path: per-block product-table images through HBM (formed by the
-// decode, then gf_mac_kernel's encode body over them) when a block spans at
-// least the ctx's MEMO_EC_OPT_IMAGE_MIN_TILES tiles and its tables are
-// costly to build per tile: R x kpad >= MEMO_EC_OPT_IMAGE_MIN_COEFS, or k
-// off the straight-line bodies (the chunk loop builds its images one per
-// lane, after the barrier).  The LDS build inside the MAC is the right call
-// for small blocks (4 KiB RS(16,4): a 2 KiB image per 5 KiB of traffic,
-// DESIGN.md 4.1); a block of T tiles builds the same images T times there,
-// against one build and R * kpad * 32 bytes of HBM per block here.
-// Measured, interleaved on one box (tools/image_ab.py):
-// RS(16,4) 128 KiB-4 MiB +2.6 to +4 points, RS(8,4) / RS(20,4) / RS(10,6)
-// +3 to +5; RS(4,2), RS(6,3), RS(10,4), RS(12,4) -0.4 to 0 (kept in LDS);
-// one-tile blocks -0.1 (RS(16,4) 64 KiB) to -60 (4 KiB).
+// column-per-lane decode beside the rows, then the encode's code over them:
+// gf_mac_images_kernel) when a shard holds at least the ctx's
+// MEMO_EC_OPT_IMAGE_MIN_TILES whole tiles and its tables are costly to build
+// per tile: R x kpad >= MEMO_EC_OPT_IMAGE_MIN_COEFS, or k off the
+// straight-line bodies (the chunk loop builds its images one per lane,
+// after the barrier).  A block of T tiles builds the same images T times in
+// LDS, against one build and R * kpad * 32 bytes of HBM per block here; below
+// one tile per shard the images cost more traffic than the build saves
+// (4 KiB RS(16,4): a 2 KiB image per 5 KiB of traffic).  Measured with
+// tools/image_ab.py: RS(16,4) 128 KiB-4 MiB +2 to +3.6
+// points, RS(10,4) / RS(12,4) 40 KiB-4 MiB -0.3 to +2.9 by box, the
+// chunk-loop codes +4 to +7; RS(4,2) and RS(6,3) (8 and 18 coefficients)
+// -0.6 to +0.1, so they keep their LDS tables.
 bool rows_images(const memo_ec_ctx* c, size_t S, int k, int R, int KC) {
   const uint64_t t = c->opt.image_min_tiles;
   if (t == 0 || S / 16 / MAC_TILE < t) return false;  // whole tiles per shard
