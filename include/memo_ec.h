@@ -147,10 +147,15 @@ enum memo_ec_option {
                                            (S / 4096) and runs the encode body
                                            over them (1; 0: never, tables built
                                            in LDS)                               */
-    MEMO_EC_OPT_IMAGE_MIN_COEFS = 12    /* MEMO_EC_IMAGE_MIN_COEFS: ... and at least
+    MEMO_EC_OPT_IMAGE_MIN_COEFS = 12,   /* MEMO_EC_IMAGE_MIN_COEFS: ... and at least
                                            this many coefficients per block
                                            (padded rows x columns; 40) or a k
                                            without a straight-line MAC body      */
+    MEMO_EC_OPT_DECODE_OVERLAP = 13     /* MEMO_EC_DECODE_OVERLAP: a mixed rebuild runs
+                                           the decode rows of its later launch
+                                           classes on a side stream, overlapping
+                                           the earlier MACs (1; 0: all decodes
+                                           first, on the call's stream)          */
 };
 
 /* Number of GPUs the library can use (0 without a GPU).  A node process

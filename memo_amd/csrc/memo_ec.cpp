@@ -38,6 +38,7 @@ struct memo_ec_opts {
   int decode_stage = 0;
   uint64_t image_min_tiles = 1;           // rows path: HBM table images from this many whole tiles
   uint64_t image_min_coefs = 40;          //   per shard and this many coefficients (R x kpad)
+  int decode_overlap = 1;                 // mixed rebuilds: later decodes on a side stream
 };
 
 struct memo_ec_ctx {
@@ -54,6 +55,10 @@ struct memo_ec_ctx {
   hipEvent_t ev_order = nullptr;
   uint32_t* d_status = nullptr;   // deferred device errors (bit 0: singular)
   uint32_t* h_status = nullptr;   // pinned copy of d_status for host-memory calls
+  // side stream for a mixed rebuild's later decodes (overlapping earlier
+  // MACs) and its events, created on first use
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> side_ev;
   uint32_t* d_tabs = nullptr;     // rebuild scratch: per-block decode rows
   size_t tabs_cap = 0;            // bytes
   struct TabEntry {
@@ -165,6 +170,10 @@ bool set_opt(memo_ec_opts& o, int opt, int64_t v) {
       if (v < 0) return false;
       o.image_min_coefs = (uint64_t)v;
       return true;
+    case MEMO_EC_OPT_DECODE_OVERLAP:
+      if (v < 0 || v > 1) return false;
+      o.decode_overlap = (int)v;
+      return true;
     default:
       return false;
   }
@@ -184,6 +193,7 @@ bool get_opt(const memo_ec_opts& o, int opt, int64_t* v) {
     case MEMO_EC_OPT_DECODE_STAGE: *v = o.decode_stage; return true;
     case MEMO_EC_OPT_IMAGE_MIN_TILES: *v = (int64_t)o.image_min_tiles; return true;
     case MEMO_EC_OPT_IMAGE_MIN_COEFS: *v = (int64_t)o.image_min_coefs; return true;
+    case MEMO_EC_OPT_DECODE_OVERLAP: *v = o.decode_overlap; return true;
     default: return false;
   }
 }
@@ -212,6 +222,7 @@ void read_env_options(memo_ec_opts& o) {
       {"MEMO_EC_DECODE_STAGE", MEMO_EC_OPT_DECODE_STAGE, 0},
       {"MEMO_EC_IMAGE_MIN_TILES", MEMO_EC_OPT_IMAGE_MIN_TILES, 0},
       {"MEMO_EC_IMAGE_MIN_COEFS", MEMO_EC_OPT_IMAGE_MIN_COEFS, 0},
+      {"MEMO_EC_DECODE_OVERLAP", MEMO_EC_OPT_DECODE_OVERLAP, 0},
   };
   for (const Env& e : kEnv) {
     const char* p = std::getenv(e.name);
@@ -448,6 +459,18 @@ int ensure_tabs(memo_ec_ctx* ctx, size_t bytes) {
   const size_t cap = std::max<size_t>(bytes, 1 << 20);
   HIPCHK(hipMalloc(&ctx->d_tabs, cap));
   ctx->tabs_cap = cap;
+  return MEMO_EC_OK;
+}
+
+// The ctx's side stream and at least n events on it (created on first use,
+// kept for the ctx's life).
+int side_events(memo_ec_ctx* ctx, size_t n) {
+  if (!ctx->side) HIPCHK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+  while (ctx->side_ev.size() < n) {
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    ctx->side_ev.push_back(e);
+  }
   return MEMO_EC_OK;
 }
 
@@ -1048,7 +1071,7 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
                           hipStream_t st, uint32_t* status) {
   std::vector<const uint8_t*> prow(ps.size(), nullptr);
   std::vector<const uint32_t*> pimg(ps.size(), nullptr);
-  std::vector<DecodeArgs> dec;
+  std::vector<DecodeArgs> dec_of(ps.size());  // per MAC_ROWS piece
   size_t off = 0, rows_total = 0;
   for (const auto& p : ps)
     if (p.mode == MAC_ROWS) rows_total += p.n * (size_t)p.e * p.k;
@@ -1059,19 +1082,16 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
     if (p.mode != MAC_ROWS) continue;
     const uint32_t* lw0 = nullptr;
     if (int rc = lw0_table(c, p.k, p.m, &lw0)) return rc;
-    dec.push_back(decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0));
+    dec_of[i] = decode_args(c, p.k, p.m, p.e, p.n, p.sidx, p.lidx, rows + off, status, lw0);
     prow[i] = rows + off;
     if (p.img) {
       uint32_t* img = reinterpret_cast<uint32_t*>(img_base + ioff);
       pimg[i] = img;
-      with_images(dec.back(), img, p.R, p.KC);
+      with_images(dec_of[i], img, p.R, p.KC);
       ioff += image_bytes(p.n, p.k, p.R, p.KC);
     }
     off += p.n * (size_t)p.e * p.k;
   }
-  // every segment's decode rows (and table images), segments of one decode
-  // kernel per launch
-  if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
   // The launch class of a piece: (mode, KC, R).  Pieces that multiply with
   // table images -- per-block images, or a shared pattern's -- join the
   // rows launch of their (KC, R) when the call has one (gf_mac_kernel's
@@ -1090,15 +1110,66 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
     if (p.img || has(p, true)) return (int)MAC_IMAGES;
     return (int)MAC_ENCODE;
   };
-  std::vector<bool> done(ps.size(), false);
-  for (size_t i = 0; i < ps.size(); ++i) {
-    if (done[i]) continue;
-    const int mode = launch_mode(ps[i]), KC = ps[i].KC, R = ps[i].R;
+  struct Cls {
+    int mode, KC, R;
+    std::vector<size_t> pieces;
+    std::vector<DecodeArgs> dec;  // the decode rows (and images) its pieces need
+  };
+  std::vector<Cls> cls;
+  {
+    std::vector<bool> done(ps.size(), false);
+    for (size_t i = 0; i < ps.size(); ++i) {
+      if (done[i]) continue;
+      Cls k{launch_mode(ps[i]), ps[i].KC, ps[i].R, {}, {}};
+      for (size_t j = i; j < ps.size(); ++j)
+        if (!done[j] && launch_mode(ps[j]) == k.mode && ps[j].KC == k.KC && ps[j].R == k.R) {
+          done[j] = true;
+          k.pieces.push_back(j);
+          if (ps[j].mode == MAC_ROWS) k.dec.push_back(dec_of[j]);
+        }
+      cls.push_back(std::move(k));
+    }
+  }
+  // Decode rows.  A call with several classes to decode (a mixed rebuild)
+  // runs the decodes of all but the first such class on the ctx's side
+  // stream, behind an event of the call's stream, so they overlap the MACs
+  // before them instead of running one after another in front of the first
+  // MAC; each class's MAC waits for its own decodes' event.  Otherwise every
+  // decode goes first on the call's stream, segments of one decode kernel
+  // per launch.
+  std::vector<int> waits(cls.size(), -1);  // class -> side-stream event
+  size_t ndec = 0;
+  for (const auto& k : cls) ndec += !k.dec.empty();
+  if (ndec > 1 && c->opt.decode_overlap) {
+    bool first = true;
+    int ne = 0;
+    for (size_t x = 0; x < cls.size(); ++x) {
+      if (cls[x].dec.empty()) continue;
+      if (first) {  // nothing runs before it to overlap with
+        HIPCHK(launch_decode_multi(cls[x].dec.data(), (int)cls[x].dec.size(), st));
+        first = false;
+        continue;
+      }
+      if (int rc = side_events(c, ne + 2)) return rc;
+      if (ne == 0) {  // the side stream starts after the call's stream's earlier work
+        HIPCHK(hipEventRecord(c->side_ev[0], st));
+        HIPCHK(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
+      }
+      HIPCHK(launch_decode_multi(cls[x].dec.data(), (int)cls[x].dec.size(), c->side));
+      HIPCHK(hipEventRecord(c->side_ev[ne + 1], c->side));
+      waits[x] = ne + 1;
+      ++ne;
+    }
+  } else {
+    std::vector<DecodeArgs> dec;
+    for (const auto& k : cls) dec.insert(dec.end(), k.dec.begin(), k.dec.end());
+    if (!dec.empty()) HIPCHK(launch_decode_multi(dec.data(), (int)dec.size(), st));
+  }
+  for (size_t x = 0; x < cls.size(); ++x) {
+    const int mode = cls[x].mode, KC = cls[x].KC, R = cls[x].R;
     std::vector<Plan> plans;
-    for (size_t j = i; j < ps.size(); ++j) {
+    for (size_t j : cls[x].pieces) {
       const auto& p = ps[j];
-      if (done[j] || launch_mode(p) != mode || p.KC != KC || p.R != R) continue;
-      done[j] = true;
       const size_t step = max_blocks_per_launch(c, p.S);
       const uint32_t* lw0 = nullptr;
       if (mode == MAC_FUSED)
@@ -1130,6 +1201,7 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
         }
       }
     }
+    if (waits[x] >= 0) HIPCHK(hipStreamWaitEvent(st, c->side_ev[waits[x]], 0));
     if (int rc = launch_plans(c, plans, st)) return rc;
   }
   return MEMO_EC_OK;
@@ -1289,6 +1361,9 @@ int memo_ec_ctx_destroy(memo_ec_ctx* c) {
     for (auto ev : {c->ev_h[i], c->ev_k[i], c->ev_d[i]})
       if (ev) (void)hipEventDestroy(ev);
   if (c->ev_order) (void)hipEventDestroy(c->ev_order);
+  if (c->side) (void)hipStreamSynchronize(c->side);
+  for (auto ev : c->side_ev) (void)hipEventDestroy(ev);
+  if (c->side) (void)hipStreamDestroy(c->side);
   for (auto st : {c->sh, c->sk, c->sd})
     if (st) (void)hipStreamDestroy(st);
   if (c->own) (void)hipStreamDestroy(c->own);

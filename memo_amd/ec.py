@@ -55,7 +55,7 @@ class RebuildSegment(ctypes.Structure):
 OPTIONS = {"rebuild_path": 1, "fused_max_bytes": 2, "zero_copy_bytes": 3, "pipe_bytes": 4,
            "copy_threads": 5, "max_launch_tiles": 6, "xcd_min_tiles": 7, "decode_wide_max": 8,
            "decode_exact": 9, "decode_stage": 10, "image_min_tiles": 11,
-           "image_min_coefs": 12}
+           "image_min_coefs": 12, "decode_overlap": 13}
 MAX_REBUILD_SEGMENTS = 256
 PROBE_MODES = {"copy": 0, "read": 1, "write": 2}  # memo_ec_probe_mode
 

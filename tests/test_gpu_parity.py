@@ -1026,7 +1026,7 @@ def test_ctx_options_round_trip(codec):
     values = {"rebuild_path": 0, "fused_max_bytes": 1 << 20, "zero_copy_bytes": 0,
               "pipe_bytes": 8 << 20, "copy_threads": 2, "max_launch_tiles": 1000,
               "xcd_min_tiles": 1, "decode_wide_max": 0, "decode_exact": 0, "decode_stage": 1,
-              "image_min_tiles": 1, "image_min_coefs": 0}
+              "image_min_tiles": 1, "image_min_coefs": 0, "decode_overlap": 0}
     old = {k: codec.get_option(k) for k in values}
     with codec.options(**values):
         assert {k: codec.get_option(k) for k in values} == values
@@ -1035,7 +1035,7 @@ def test_ctx_options_round_trip(codec):
     assert {k: codec.get_option(k) for k in values} == old
     for name, bad in [("rebuild_path", 2), ("rebuild_path", -2), ("pipe_bytes", 1000),
                       ("decode_exact", 3), ("copy_threads", -1), ("image_min_tiles", -1),
-                      ("image_min_coefs", -1)]:
+                      ("image_min_coefs", -1), ("decode_overlap", 2), ("decode_overlap", -1)]:
         with pytest.raises(ec.MemoECError) as ei:
             codec.set_option(name, bad)
         assert ei.value.code == -1
@@ -1071,6 +1071,11 @@ def test_env_options_keep_their_meanings(monkeypatch, capfd):
     monkeypatch.delenv("MEMO_EC_IMAGE_MIN_COEFS")
     with ec.Codec(0) as c:
         assert (c.get_option("image_min_tiles"), c.get_option("image_min_coefs")) == (1, 40)
+        assert c.get_option("decode_overlap") == 1
+    monkeypatch.setenv("MEMO_EC_DECODE_OVERLAP", "0")
+    with ec.Codec(0) as c:
+        assert c.get_option("decode_overlap") == 0
+    monkeypatch.delenv("MEMO_EC_DECODE_OVERLAP")
     monkeypatch.setenv("MEMO_EC_COPY_THREADS", "0")
     with ec.Codec(0) as c:
         assert c.get_option("copy_threads") == 1

@@ -224,3 +224,54 @@ def test_random_segments_vs_oracle(codec, O, seed, rebuild_path):
     codec.synchronize()
     for gi, (g, s) in enumerate(zip(groups, segs)):
         assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (seed, gi, spec[gi])
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_mixed_decode_overlap(codec, O, overlap, rebuild_path):
+    """A mixed call's later decode launches on the ctx's side stream
+    (decode_overlap = 1, the default) and all decodes first on the call's
+    stream (0): same shards, for classes with rows, images and shared
+    patterns, on back-to-back calls that reuse the scratch and events."""
+    spec = C5_MIX + [(6, 3, 4096, 30, 3, False), (12, 5, 70000, 3, 5, False), (20, 4, 300000, 2, 4, False)]
+    with codec.options(decode_overlap=overlap):
+        for seed in (11, 12):
+            groups = make_groups(O, spec, seed)
+            segs = device_segs(groups)
+            codec.rebuild_segments(segs)
+            codec.rebuild_segments(segs)  # the second call waits for the first's MACs
+            codec.synchronize()
+            for g, s in zip(groups, segs):
+                assert np.array_equal(s["out"].cpu().numpy(), g["want"]), (seed, g["k"], g["m"], g["S"], g["e"])
+
+
+def test_mixed_rebuild_graph_capture(codec, O):
+    """A mixed device-resident call captured into a HIP graph: the side
+    stream's decodes fork from and join the captured stream, and replays on
+    new survivors rebuild the new shards."""
+    import torch
+    spec = [(4, 2, 4096, 60, 2, False), (10, 4, 65536, 9, 4, False), (16, 4, 1 << 20, 3, 4, False),
+            (10, 4, 4096, 40, 1, False)]
+    groups = make_groups(O, spec, 21)
+    segs = device_segs(groups)
+    st = torch.cuda.Stream()
+    with torch.cuda.stream(st):
+        codec.set_stream(st)
+        codec.rebuild_segments(segs)  # warm-up: scratch, side stream, events
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        codec.set_stream(torch.cuda.current_stream())
+        codec.rebuild_segments(segs)
+    codec.set_stream(None)
+    for seed in (22, 23):
+        fresh = make_groups(O, spec, seed)
+        for f, s in zip(fresh, segs):
+            s["surv"].copy_(dev(f["surv"]))
+            s["surv_idx"].copy_(dev(f["s"]))
+            s["lost_idx"].copy_(dev(f["l"]))
+            s["out"].zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        for f, s in zip(fresh, segs):
+            assert np.array_equal(s["out"].cpu().numpy(), f["want"]), (seed, f["k"], f["S"])
