@@ -229,11 +229,23 @@ def test_random_segments_vs_oracle(codec, O, seed, rebuild_path):
 @pytest.mark.parametrize("overlap", [0, 1])
 def test_mixed_decode_overlap(codec, O, overlap, rebuild_path):
     """A mixed call's later decode launches on the ctx's side stream
-    (decode_overlap = 1, the default) and all decodes first on the call's
+    (decode_overlap = 1, the default) or all decodes first on the call's
     stream (0): same shards, for classes with rows, images and shared
-    patterns, on back-to-back calls that reuse the scratch and events."""
+    patterns, on back-to-back calls that reuse the scratch and events; the
+    encode of the same groups beside them."""
     spec = C5_MIX + [(6, 3, 4096, 30, 3, False), (12, 5, 70000, 3, 5, False), (20, 4, 300000, 2, 4, False)]
     with codec.options(decode_overlap=overlap):
+        enc = []
+        for gi, (k, m, B, n, e, uni) in enumerate(spec):
+            S = O.shard_size(B, k)
+            data = O.fill_blocks(SEED, 31 * gi, n, B, k, S)
+            enc.append((k, m, S, n, dev(data), empty(n, m * S), O.encode(k, m, S, data, threads=4)))
+        for _ in range(2):
+            for i in range(0, len(enc), 12):  # MEMO_EC_MAX_SEGMENTS per encode call
+                codec.encode_segments([x[:6] for x in enc[i:i + 12]])
+        codec.synchronize()
+        for gi, x in enumerate(enc):
+            assert np.array_equal(x[5].cpu().numpy(), x[6]), (gi, spec[gi])
         for seed in (11, 12):
             groups = make_groups(O, spec, seed)
             segs = device_segs(groups)

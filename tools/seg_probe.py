@@ -3,6 +3,7 @@
 rebuild_segments call, timed with HIP events (run under rocprofv3
 --kernel-trace for the launches inside each call).  Prints one JSON line."""
 import json
+import os
 import sys
 
 import numpy as np
@@ -15,6 +16,9 @@ if len(sys.argv) > 3:  # another build of the library (an A/B's other side)
     ec.LIB_PATH = sys.argv[3]
 
 SEED = 0x6D656D6F
+# untimed calls before each timed series; ~150 settle the clocks (the ramp
+# after a load step: profiles/HISTORY.md "Clock ramp")
+WARMUP = int(os.environ.get("SEG_PROBE_WARMUP", "5"))
 
 
 def main():
@@ -48,7 +52,7 @@ def main():
             res = {"rep": rep}
             for name, fn, nbytes in [("encode", lambda: c.encode_segments(segs), alg),
                                      ("rebuild", lambda: c.rebuild_segments(rsegs), ralg)]:
-                for _ in range(5):
+                for _ in range(WARMUP):
                     fn()
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
                 ev[0].record(st)
