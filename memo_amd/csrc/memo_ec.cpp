@@ -1138,6 +1138,16 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
   // decode goes first on the call's stream, segments of one decode kernel
   // per launch.
   std::vector<int> waits(cls.size(), -1);  // class -> side-stream event
+  // On an early return st still waits for the side stream's last decode,
+  // so a later call cannot reuse the scratch while that decode runs.
+  struct SideJoin {
+    memo_ec_ctx* c;
+    hipStream_t st;
+    int last = -1;  // side event st has not waited for yet
+    ~SideJoin() {
+      if (last >= 0) (void)hipStreamWaitEvent(st, c->side_ev[last], 0);
+    }
+  } join{c, st};
   size_t ndec = 0;
   for (const auto& k : cls) ndec += !k.dec.empty();
   if (ndec > 1 && c->opt.decode_overlap) {
@@ -1157,7 +1167,7 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
       }
       HIPCHK(launch_decode_multi(cls[x].dec.data(), (int)cls[x].dec.size(), c->side));
       HIPCHK(hipEventRecord(c->side_ev[ne + 1], c->side));
-      waits[x] = ne + 1;
+      waits[x] = join.last = ne + 1;
       ++ne;
     }
   } else {
@@ -1201,7 +1211,10 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
         }
       }
     }
-    if (waits[x] >= 0) HIPCHK(hipStreamWaitEvent(st, c->side_ev[waits[x]], 0));
+    if (waits[x] >= 0) {
+      HIPCHK(hipStreamWaitEvent(st, c->side_ev[waits[x]], 0));
+      if (waits[x] == join.last) join.last = -1;
+    }
     if (int rc = launch_plans(c, plans, st)) return rc;
   }
   return MEMO_EC_OK;
