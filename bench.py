@@ -299,6 +299,14 @@ C5_CODES = [(4, 2), (10, 4), (16, 4)]
 C5_SIZES = [4 << 10, 64 << 10, 1 << 20, 4 << 20]
 
 
+def side_stream_decodes(ec, codec):
+    """The ctx's MEMO_EC_OPT_DECODE_OVERLAP (None: a library without it)."""
+    try:
+        return bool(codec.get_option("decode_overlap"))
+    except (ec.MemoECError, KeyError):
+        return None
+
+
 def c5_mixed(torch, ec, codec, stream, gib, steps, warmup, settle_ms, stage=None, threads=1):
     """BASELINE.json C5 as the plugin issues it: 12 groups, (k,m) in
     {(4,2),(10,4),(16,4)} x B in {4 KiB, 64 KiB, 1 MiB, 4 MiB}, ~gib GiB of
@@ -352,7 +360,8 @@ def c5_mixed(torch, ec, codec, stream, gib, steps, warmup, settle_ms, stage=None
            "encode": {"kernel_ms": round(ms, 4), "GiBs": round(pay / (ms * 1e-3) / 2**30, 1),
                       "frac": frac(alg, ms), "bytes_per_call": alg},
            "rebuild": {"step_ms": round(rs, 4), "GiBs": round(pay / (rs * 1e-3) / 2**30, 1),
-                       "frac": frac(ralg, rs), "bytes_per_call": ralg},
+                       "frac": frac(ralg, rs), "bytes_per_call": ralg,
+                       "side_stream_decodes": side_stream_decodes(ec, codec)},
            "encode_rebuild_GiBs": round(2 * pay / ((ms + rs) * 1e-3) / 2**30, 1)}
     per = []
     for g in groups:
