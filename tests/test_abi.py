@@ -21,6 +21,15 @@ def test_header_and_binding_agree():
     assert sorted(ec.EXPORTS) == header_symbols()
 
 
+def test_option_ids_agree_with_header():
+    """memo_amd.ec.OPTIONS names every memo_ec_option of the header, with
+    the header's value (MEMO_EC_OPT_IMAGE_MIN_TILES -> "image_min_tiles")."""
+    from memo_amd import ec
+    txt = open(os.path.join(ROOT, "include", "memo_ec.h")).read()
+    hdr = {n.lower(): int(v) for n, v in re.findall(r"\bMEMO_EC_OPT_([A-Z0-9_]+)\s*=\s*(\d+)", txt)}
+    assert hdr and ec.OPTIONS == hdr
+
+
 def test_library_exports_every_header_symbol():
     from memo_amd import ec
     lib = ctypes.CDLL(ec.LIB_PATH)
