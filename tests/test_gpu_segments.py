@@ -175,6 +175,33 @@ def test_segments_bad_patterns(codec, O, rebuild_path):
     codec.synchronize()
 
 
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_bad_pattern_in_a_later_class(codec, O, overlap, rebuild_path):
+    """A faulty survivor set in a class whose decode runs on the side stream
+    (not the call's first class): its block is zeroed, the fault is still
+    reported at synchronize, and every other block and segment is rebuilt."""
+    from memo_amd import ec
+    groups = make_groups(O, [(4, 2, 65536, 3, 2, False), (10, 4, 4096, 6, 2, False),
+                             (16, 4, 1 << 20, 2, 4, False)], 15)
+    bad = groups[1]["s"].copy()
+    bad[4, 2] = bad[4, 3]
+    segs = device_segs(groups)
+    segs[1]["surv_idx"] = dev(bad)
+    with codec.options(decode_overlap=overlap):
+        codec.rebuild_segments(segs)
+        with pytest.raises(ec.MemoECError) as ei:
+            codec.synchronize()
+    assert ei.value.code == -4
+    got = segs[1]["out"].cpu().numpy()
+    good = np.ones(6, bool)
+    good[4] = False
+    assert not got[4].any()
+    assert np.array_equal(got[good], groups[1]["want"][good])
+    for i in (0, 2):
+        assert np.array_equal(segs[i]["out"].cpu().numpy(), groups[i]["want"]), i
+    codec.synchronize()
+
+
 @pytest.mark.parametrize("spec", [
     # k outside the straight-line bodies (chunk loop), k > 16, m > 4 (R > 4)
     [(3, 2, 5000, 9, 2, False), (5, 3, 4096, 20, 3, False), (7, 3, 70000, 4, 1, True),
