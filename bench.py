@@ -900,28 +900,61 @@ PLUGIN_BIN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "host", "_
 # eviction + repair) beside replication; a few seconds each.
 PLUGIN_SIZES = [(16384, 4096), (512, 1 << 20)]
 PLUGIN_KEYS = ("store_GiBs", "fetch_GiBs", "degraded_fetch_GiBs", "repair_GiBs")
+PLUGIN_REPS = 5
 
 
-def plugin_lines(binary=PLUGIN_BIN, sizes=PLUGIN_SIZES, timeout=240):
+def spread(samples):
+    """{median, min, max, n, samples} of one rate's repetitions."""
+    v = sorted(float(x) for x in samples)
+    n = len(v)
+    med = v[n // 2] if n % 2 else (v[n // 2 - 1] + v[n // 2]) / 2
+    return {"median": round(med, 3), "min": round(v[0], 3), "max": round(v[-1], 3), "n": n,
+            "samples": [round(float(x), 3) for x in samples]}
+
+
+def plugin_aggregate(d):
+    """The child's per-repetition lists -> {median, min, max, n} per rate, and
+    the erasure / replication ratio of each repetition (the two ran
+    back to back in that repetition, so the ratio cancels box drift) for
+    store and fetch."""
+    er, rp = dict(d.get("erasure", {})), dict(d.get("replication", {}))
+    for side in (er, rp):
+        for key, val in list(side.items()):
+            if key.endswith("_GiBs") and isinstance(val, list) and val:
+                side[key] = spread(val)
+    ratio = {}
+    for key in ("store_GiBs", "fetch_GiBs"):
+        a, b = er.get(key), rp.get(key)
+        if isinstance(a, dict) and isinstance(b, dict) and a["n"] == b["n"]:
+            per = [x / y for x, y in zip(a["samples"], b["samples"]) if y > 0]
+            if len(per) == a["n"]:
+                ratio[key.replace("_GiBs", "")] = spread(per)
+    return er, rp, ratio
+
+
+def plugin_lines(binary=PLUGIN_BIN, sizes=PLUGIN_SIZES, timeout=240, reps=PLUGIN_REPS):
     """The plugin level (host/erasure_consensus.cc, the drop-in for the
     reference's Consensus, src/memo/model/doughnut/Consensus.hh:24-174): child runs
     of host/tests/bench_plugin.cc, each on in-process memory-silo nodes, which
     exit non-zero unless every healthy, degraded and post-repair fetch returns
     bytes whose SHA-256 matches the block's CHB address and nothing is left
-    unrecoverable.  Host-bound (the place step and silo copies), not a kernel
-    roofline line; it runs after the timed region."""
+    unrecoverable.  Each child runs erasure and replication interleaved `reps`
+    times on fresh nodes; a row carries {median, min, max, n} per rate and
+    the per-repetition erasure / replication ratios (`ratio`).  Host-bound
+    (the place step and silo copies), not a kernel roofline line; it runs
+    after the timed region."""
     import subprocess
     out = {}
     for nb, bb in sizes:
         key = "%dx%d" % (nb, bb)
         try:
-            r = subprocess.run([binary, str(nb), str(bb)], stdout=subprocess.PIPE,
+            r = subprocess.run([binary, str(nb), str(bb), str(reps)], stdout=subprocess.PIPE,
                                stderr=subprocess.PIPE, timeout=timeout)
             line = r.stdout.decode(errors="replace").strip().splitlines()
             d = json.loads(line[-1]) if line else {}
-            er, rp = d.get("erasure", {}), d.get("replication", {})
+            er, rp, ratio = plugin_aggregate(d)
             row = {"ok": r.returncode == 0 and all(x in er for x in PLUGIN_KEYS),
-                   "erasure": er, "replication": rp}
+                   "reps": d.get("reps"), "erasure": er, "replication": rp, "ratio": ratio}
             if not row["ok"]:
                 row["note"] = "rc %d: %s" % (r.returncode, r.stderr.decode(errors="replace")[-300:])
         except (OSError, subprocess.SubprocessError, ValueError, IndexError) as ex:

@@ -334,26 +334,29 @@ uint32_t shard_crc(const uint8_t* wire, size_t S) {
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload) { return encode_shard(h, payload, h.index); }
 
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload, int index) {
+  Buffer w(ShardHeader::kSize + h.shard_size);
+  frame_shard(h, payload, index, w.data());
+  return w;
+}
+
+void frame_shard(const ShardHeader& h, const uint8_t* payload, int index, uint8_t* w) {
   if (h.salt.size() > 32) throw Error("shard: salt longer than 32 bytes");
-  Buffer w;
-  w.reserve(ShardHeader::kSize + h.shard_size);
-  w.resize(ShardHeader::kSize, 0);
-  w.insert(w.end(), payload, payload + h.shard_size);
-  std::memcpy(w.data(), "MECS", 4);
+  std::memset(w, 0, ShardHeader::kSize);
+  std::memcpy(w + ShardHeader::kSize, payload, h.shard_size);
+  std::memcpy(w, "MECS", 4);
   w[4] = ShardHeader::kVersion;
   w[5] = h.k;
   w[6] = h.m;
   w[7] = (uint8_t)index;
-  std::memcpy(w.data() + 8, &h.block_size, 8);
-  std::memcpy(w.data() + 16, &h.shard_size, 8);
-  std::memcpy(w.data() + 24, h.address.value.data(), 32);
+  std::memcpy(w + 8, &h.block_size, 8);
+  std::memcpy(w + 16, &h.shard_size, 8);
+  std::memcpy(w + 24, h.address.value.data(), 32);
   const uint32_t sl = (uint32_t)h.salt.size();
-  std::memcpy(w.data() + 56, &sl, 4);
-  if (sl) std::memcpy(w.data() + 60, h.salt.data(), sl);
-  std::memcpy(w.data() + 92, h.owner.value.data(), 32);
-  const uint32_t crc = shard_crc(w.data(), h.shard_size);
-  std::memcpy(w.data() + kCrcAt, &crc, 4);
-  return w;
+  std::memcpy(w + 56, &sl, 4);
+  if (sl) std::memcpy(w + 60, h.salt.data(), sl);
+  std::memcpy(w + 92, h.owner.value.data(), 32);
+  const uint32_t crc = shard_crc(w, h.shard_size);
+  std::memcpy(w + kCrcAt, &crc, 4);
 }
 
 ShardHeader decode_shard_header(const uint8_t* w, size_t n) {
@@ -379,31 +382,16 @@ ShardHeader decode_shard_header(const uint8_t* w, size_t n) {
   return h;
 }
 
-ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
-  if (w.size() < ShardHeader::kSize || std::memcmp(w.data(), "MECS", 4) != 0)
-    throw ValidationFailed("shard: bad magic");
-  ShardHeader h;
-  h.version = w[4];
-  h.k = w[5];
-  h.m = w[6];
-  h.index = w[7];
-  std::memcpy(&h.block_size, w.data() + 8, 8);
-  std::memcpy(&h.shard_size, w.data() + 16, 8);
-  h.address = Address(w.data() + 24, 0, false);
-  uint32_t sl;
-  std::memcpy(&sl, w.data() + 56, 4);
-  if (h.version != ShardHeader::kVersion) throw ValidationFailed("shard: unknown version");
-  if (sl > 32) throw ValidationFailed("shard: bad salt length");
-  h.salt.assign(w.begin() + 60, w.begin() + 60 + sl);
-  h.owner = Address(w.data() + 92, 0, false);
-  std::memcpy(&h.crc, w.data() + kCrcAt, 4);
-  if (h.k < 1 || h.index >= h.k + h.m) throw ValidationFailed("shard: bad geometry");
-  if (h.shard_size != memo_ec_shard_size(h.block_size, h.k))
-    throw ValidationFailed("shard: size does not match block size");
-  if (w.size() != ShardHeader::kSize + h.shard_size) throw ValidationFailed("shard: truncated");
-  if (shard_crc(w.data(), h.shard_size) != h.crc) throw ValidationFailed("shard: checksum mismatch");
-  if (payload) *payload = w.data() + ShardHeader::kSize;
+ShardHeader decode_shard_view(const uint8_t* w, size_t n, const uint8_t** payload) {
+  ShardHeader h = decode_shard_header(w, n);
+  if (n != ShardHeader::kSize + h.shard_size) throw ValidationFailed("shard: truncated");
+  if (shard_crc(w, h.shard_size) != h.crc) throw ValidationFailed("shard: checksum mismatch");
+  if (payload) *payload = w + ShardHeader::kSize;
   return h;
+}
+
+ShardHeader decode_shard(const Buffer& w, const uint8_t** payload) {
+  return decode_shard_view(w.data(), w.size(), payload);
 }
 
 ShardKeys::ShardKeys(const Address& a) {
@@ -448,8 +436,8 @@ void ThreadPool::worker() {
 }
 
 // Items are claimed from a shared counter by up to `threads` pool tasks and
-// by the calling thread itself, so n tiny items cost n atomic increments, not
-// n queue round trips.  The caller returns once every item has run; tasks
+// by the calling thread itself, so n tiny items cost a few atomic increments
+// per thread, not n queue round trips.  The caller returns once every item has run; tasks
 // that start late find no item left and only drop their reference to the
 // shared state.
 void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
@@ -463,18 +451,23 @@ void ThreadPool::parallel_for(size_t n, const std::function<void(size_t)>& fn) {
   };
   auto st = std::make_shared<State>();
   const std::function<void(size_t)>* f = &fn;
-  auto work = [st, f, n] {
+  // items are claimed `grain` at a time: about 8 claims per thread, so that
+  // thousands of small items do not all meet on the shared counter's line
+  const size_t grain = std::max<size_t>(1, n / (8 * (ts_.size() + 1)));
+  auto work = [st, f, n, grain] {
     size_t mine = 0;
     for (;;) {
-      const size_t i = st->next.fetch_add(1);
-      if (i >= n) break;
-      try {
-        (*f)(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(st->dm);
-        if (!st->err) st->err = std::current_exception();
+      const size_t i0 = st->next.fetch_add(grain);
+      if (i0 >= n) break;
+      for (size_t i = i0; i < std::min(n, i0 + grain); ++i) {
+        try {
+          (*f)(i);
+        } catch (...) {
+          std::lock_guard<std::mutex> g(st->dm);
+          if (!st->err) st->err = std::current_exception();
+        }
+        ++mine;
       }
-      ++mine;
     }
     if (mine) {
       std::lock_guard<std::mutex> g(st->dm);
@@ -543,7 +536,72 @@ ErasureConsensus::~ErasureConsensus() {
   bthread_.join();
 }
 
-std::string ErasureConsensus::redundancy() const {
+// ------------------------------------------------------------ shard peer
+ShardLocal::ShardLocal(std::unique_ptr<Local> backend) : Local(*backend), backend_(std::move(backend)) {}
+
+void ShardLocal::validate(const Key& k, const uint8_t* v, size_t n) const {
+  if (n < 4 || std::memcmp(v, "MECS", 4) != 0) return backend_->validate(k, v, n);
+  const ShardHeader h = decode_shard_view(v, n, nullptr);  // geometry, size, CRC32C
+  if (shard_key(h.address, h.index) != k) throw ValidationFailed("shard: stored under a foreign key");
+  // validate with the previous value, if any: a shard replaces a shard only
+  // (a repair rewriting a damaged copy), never another kind of value
+  bool other = false;
+  auto prev = [&](const uint8_t* p, size_t pn) { other = pn < 4 || std::memcmp(p, "MECS", 4) != 0; };
+  if (storage().read(k, prev) && other) throw ValidationFailed("shard: key holds another kind of value");
+}
+
+std::unique_ptr<Local> make_shard_local(std::unique_ptr<Silo> storage) {
+  return std::make_unique<ShardLocal>(make_replica_local(std::move(storage)));
+}
+
+std::unique_ptr<Local> ErasureConsensus::make_local(std::optional<int> port,
+                                                    std::optional<IpAddress> listen_address,
+                                                    std::unique_ptr<Silo> storage) {
+  return std::make_unique<ShardLocal>(backend_->make_local(port, std::move(listen_address), std::move(storage)));
+}
+
+namespace {
+struct ErasureStat : Consensus::Stat {
+  std::string text;
+  std::string json() const override { return text; }
+};
+}  // namespace
+
+std::unique_ptr<Consensus::Stat> ErasureConsensus::stat(const Address& a) {
+  auto st = std::make_unique<ErasureStat>();
+  if (a.mutable_block()) {
+    auto b = backend_->stat(a);
+    st->text = b->json();
+    return st;
+  }
+  Placement pl;
+  bool placed = false;
+  {
+    std::shared_lock<std::shared_mutex> g(index_mu_);
+    auto it = index_.find(a);
+    if (it != index_.end()) {
+      pl = it->second;
+      placed = true;
+    }
+  }
+  std::string holders;
+  int reachable = 0;
+  for (size_t i = 0; i < pl.holder.size(); ++i) {
+    holders += std::string(i ? " " : "") + (pl.holder[i] ? pl.holder[i].hex() : "-");
+    if (pl.holder[i])
+      if (auto nd = overlay_.node(pl.holder[i]))
+        reachable += nd->up && !nd->evicted;
+  }
+  st->text = to_json({{"placed", placed ? "1" : "0"},
+                      {"k", std::to_string(o_.k)},
+                      {"m", std::to_string(o_.m)},
+                      {"block_size", std::to_string(pl.B)},
+                      {"holders", holders},
+                      {"reachable", std::to_string(reachable)}});
+  return st;
+}
+
+std::string ErasureConsensus::redundancy() {
   char f[32];
   std::snprintf(f, sizeof f, "%.4g", double(o_.k + o_.m) / o_.k);
   return to_json({{"type", "erasure"},
@@ -560,7 +618,9 @@ size_t ErasureConsensus::under_placed() const {
   return n;
 }
 
-std::string ErasureConsensus::stats() const {
+std::string ErasureConsensus::stats() { return stats_text(); }
+
+std::string ErasureConsensus::stats_text() const {
   size_t blocks, under = 0;
   std::string sample;
   {
@@ -577,9 +637,9 @@ std::string ErasureConsensus::stats() const {
                   {"under_placed", std::to_string(under)},
                   {"sample_under_placed", sample},
                   {"segments_calls", std::to_string(codec_.segments_calls())},
-                  {"stored", std::to_string(stored_)},
-                  {"fetched", std::to_string(fetched_)},
-                  {"decoded", std::to_string(decoded_)},
+                  {"stored", std::to_string(stored_.load())},
+                  {"fetched", std::to_string(fetched_.load())},
+                  {"decoded", std::to_string(decoded_.load())},
                   {"repaired", std::to_string(repaired_)},
                   {"evictions", std::to_string(evictions_)},
                   {"subset_recoveries", std::to_string(subset_recoveries_)},
@@ -849,21 +909,48 @@ std::exception_ptr ErasureConsensus::place_batch(const std::vector<const Block*>
     for (size_t o = 0; o < v.size(); o += run) tasks.push_back({nd, {v.data() + o, std::min(run, v.size() - o)}});
   std::vector<uint8_t> ok(n * total, 0);
   tm.lap("group");
+  // Small shards are framed a run at a time into one buffer (up to
+  // kFrameRunBytes) that the run's silo values share: one allocation per
+  // run instead of one per shard.  Large shards keep a buffer each (a
+  // shared run would stay allocated until its last shard is erased).
+  const size_t W = ShardHeader::kSize + S;
+  const size_t per_frame = W <= kFrameShardMax ? std::max<size_t>(1, kFrameRunBytes / W) : 0;
   pool_.parallel_for(tasks.size(), [&](size_t t) {
     Node* nd = tasks[t].first;
     const auto [e0, ne] = tasks[t].second;
-    for (size_t x = 0; x < ne; ++x) {
-      const uint32_t e = e0[x];
+    auto payload = [&](uint32_t e) {
       const size_t i = e / total;
       const int j = (int)(e % total);
-      const uint8_t* p = j < k ? data + (i * k + j) * S : parity + (i * m + (j - k)) * S;
-      try {
-        nd->store((*keys[i])(j), encode_shard(hdr[i], p, j));
-        ok[e] = 1;
-      } catch (Error&) {
-        // unreachable (Unavailable) or refused (silo::InsufficientSpace, ...):
-        // a shard not placed, so the placement below records what did land
+      return j < k ? data + (i * k + j) * S : parity + (i * m + (j - k)) * S;
+    };
+    for (size_t x0 = 0; x0 < ne;) {
+      const size_t cnt = per_frame ? std::min(per_frame, ne - x0) : 1;
+      std::shared_ptr<uint8_t> run;
+      if (per_frame) {
+        run.reset(new uint8_t[cnt * W], std::default_delete<uint8_t[]>());
+        for (size_t x = 0; x < cnt; ++x) {
+          const uint32_t e = e0[x0 + x];
+          frame_shard(hdr[e / total], payload(e), (int)(e % total), run.get() + x * W);
+        }
       }
+      for (size_t x = 0; x < cnt; ++x) {
+        const uint32_t e = e0[x0 + x];
+        const size_t i = e / total;
+        const int j = (int)(e % total);
+        try {
+          // a slot is W bytes; the block's own shard may be smaller (a batch
+          // mixes shard sizes within one bucket)
+          if (per_frame)
+            nd->store_shared((*keys[i])(j), std::shared_ptr<const uint8_t>(run, run.get() + x * W),
+                             ShardHeader::kSize + hdr[i].shard_size);
+          else nd->store((*keys[i])(j), encode_shard(hdr[i], payload(e), j));
+          ok[e] = 1;
+        } catch (Error&) {
+          // unreachable (Unavailable) or refused (silo::InsufficientSpace, ...):
+          // a shard not placed, so the placement below records what did land
+        }
+      }
+      x0 += cnt;
     }
   });
   tm.lap("stores");
@@ -925,8 +1012,15 @@ void ErasureConsensus::commit_placements(std::vector<Placed>& placed) {
     for (auto& a : under) post(kUnderPlaced, a);
 }
 
-void ErasureConsensus::_store(const Block& b, StoreMode mode) {
-  if (b.is_mutable || b.address.mutable_block()) return backend_->store(b, mode);
+void ErasureConsensus::_store(std::unique_ptr<Block> block, StoreMode mode,
+                              std::unique_ptr<ConflictResolver> resolver) {
+  if (!block) throw Error("erasure: store of a null block");
+  if (block->is_mutable || block->address.mutable_block())
+    return backend_->store(std::move(block), mode, std::move(resolver));
+  store_one(*block);
+}
+
+void ErasureConsensus::store_one(const Block& b) {
   if (!chb_valid(b.address, b.salt, b.owner, b.data)) throw ValidationFailed("CHB address mismatch");
   EncodeJob job{&b, {}};
   auto fut = job.parity.get_future();
@@ -942,7 +1036,7 @@ void ErasureConsensus::_store(const Block& b, StoreMode mode) {
 void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
   std::vector<const Block*> imm;
   for (auto& b : blocks) {
-    if (b.is_mutable || b.address.mutable_block()) backend_->store(b, STORE_INSERT);
+    if (b.is_mutable || b.address.mutable_block()) backend_->store(std::make_unique<Block>(b), STORE_INSERT, nullptr);
     else imm.push_back(&b);
   }
   // Chunks of up to stage_bytes of shards: the per-block host work (CHB
@@ -1003,61 +1097,87 @@ void ErasureConsensus::store_many(const std::vector<Block>& blocks) {
 // Then, for blocks this client did not place or shards that moved, from
 // every node in lookup order, in waves.  parallel = false works node by
 // node (for callers already on the pool).
+// With `block`, the payloads of data shards are validated on the silo's
+// view and copied straight into their slots of *block (k x S, allocated on
+// the first accepted shard); their entries in the result carry no bytes.
+// Parity shards always come back whole (header + payload).
 std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Address& a, int want,
                                                                     bool& any_down,
                                                                     ShardHeader* hdr,
                                                                     bool parallel,
-                                                                    std::vector<Node*>* from) {
-  const int total = o_.k + o_.m;
+                                                                    std::vector<Node*>* from,
+                                                                    Buffer* block) {
+  const int k = o_.k, total = o_.k + o_.m;
   // the shard keys (one SHA-256 for the block), outside the parallel fetches
-  std::vector<Key> keys(total);
+  std::array<Key, MEMO_EC_MAX_K + MEMO_EC_MAX_M> keys;
   {
     const ShardKeys sk(a);
     for (int i = 0; i < total; ++i) keys[i] = sk(i);
   }
-  std::map<int, Buffer> got;
+  // shards in hand: got[i], their wire bytes in wires[i] (none for a data
+  // shard copied into *block)
+  std::array<char, MEMO_EC_MAX_K + MEMO_EC_MAX_M> got{};
+  std::array<Buffer, MEMO_EC_MAX_K + MEMO_EC_MAX_M> wires;
+  int ngot = 0;
   std::mutex gm;
   bool have_ref = false;
   ShardHeader ref;
   any_down = false;
   auto have = [&](int i) {
     std::lock_guard<std::mutex> g(gm);
-    return got.count(i) != 0;
+    return got[i] != 0;
   };
   auto count = [&] {
     std::lock_guard<std::mutex> g(gm);
-    return (int)got.size();
+    return ngot;
   };
   // fetch shard i from nd; true if the node was reachable
   auto try_node = [&](const std::shared_ptr<Node>& nd, int i) -> bool {
-    Buffer wire;
+    auto accept = [&](const uint8_t* w, size_t n) {
+      const uint8_t* pay = nullptr;
+      ShardHeader h;
+      try {
+        h = decode_shard_view(w, n, &pay);
+      } catch (ValidationFailed&) {
+        return;  // corrupted shard: an erasure
+      }
+      if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) return;
+      uint8_t* slot = nullptr;
+      bool in_block = false;
+      {
+        std::lock_guard<std::mutex> g(gm);
+        if (!have_ref) {
+          ref = h;
+          have_ref = true;
+        } else if (!h.same_block(ref)) {
+          return;  // another geometry, salt or owner: an erasure
+        }
+        if (got[i]) return;
+        got[i] = 1;
+        ++ngot;
+        if (from) (*from)[i] = nd.get();
+        if (block && i < k) {
+          if (block->empty()) block->resize((size_t)k * ref.shard_size);
+          slot = block->data() + (size_t)i * ref.shard_size;  // claimed: this thread's alone
+          in_block = true;
+        }
+      }
+      if (!in_block) wires[i].assign(w, w + n);
+      else if (h.shard_size) std::memcpy(slot, pay, h.shard_size);
+    };
     try {
       // in flight from this client (Paxos.cc:506-507), for the ordering below
-      std::atomic<int>& tr = transfers(nd.get());
-      tr.fetch_add(1, std::memory_order_relaxed);
+      Counter& tr = transfers(nd.get());
+      tr.add(1);
       struct Done {
-        std::atomic<int>& t;
-        ~Done() { t.fetch_sub(1, std::memory_order_relaxed); }
+        Counter& t;
+        ~Done() { t.add(-1); }
       } done{tr};
-      if (!nd->try_fetch(keys[i], wire)) return true;
+      nd->try_read(keys[i], accept);
     } catch (Unavailable&) {
       std::lock_guard<std::mutex> g(gm);
       any_down = true;
       return false;
-    }
-    try {
-      ShardHeader h = decode_shard(wire, nullptr);
-      if (h.address != a || h.index != i || h.k != o_.k || h.m != o_.m) return true;
-      std::lock_guard<std::mutex> g(gm);
-      if (!have_ref) {
-        ref = h;
-        have_ref = true;
-      } else if (!h.same_block(ref)) {
-        return true;  // another geometry, salt or owner: an erasure
-      }
-      if (got.emplace(i, std::move(wire)).second && from) (*from)[i] = nd.get();
-    } catch (ValidationFailed&) {
-      // corrupted shard: an erasure
     }
     return true;
   };
@@ -1110,7 +1230,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
       thread_local std::mt19937_64 rng(std::random_device{}());
       std::shuffle(ids.begin(), ids.end(), rng);
       std::vector<std::pair<int, int>> load;
-      for (int i : ids) load.push_back({transfers(holder[i].get()).load(std::memory_order_relaxed), i});
+      for (int i : ids) load.push_back({(int)transfers(holder[i].get()).load(), i});
       std::stable_sort(load.begin(), load.end(),
                        [](const auto& x, const auto& y) { return x.first < y.first; });
       for (size_t t = 0; t < ids.size(); ++t) ids[t] = load[t].second;
@@ -1147,7 +1267,9 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   }
   if (hdr && have_ref) *hdr = ref;
   std::vector<std::pair<int, Buffer>> out;
-  for (auto& kv : got) out.emplace_back(kv.first, std::move(kv.second));
+  out.reserve(ngot);
+  for (int i = 0; i < total; ++i)
+    if (got[i]) out.emplace_back(i, std::move(wires[i]));
   return out;
 }
 
@@ -1156,7 +1278,7 @@ ErasureConsensus::Gathered ErasureConsensus::collect(const Address& a, bool para
   const int k = o_.k;
   try {
     bool any_down = false;
-    g.shards = gather_shards(a, k, any_down, &g.h, parallel);
+    g.shards = gather_shards(a, k, any_down, &g.h, parallel, nullptr, &g.block);
     if (g.shards.empty()) {
       if (any_down) throw TooFewPeers("erasure: no shard reachable for " + a.hex());
       throw MissingBlock("missing block " + a.hex());
@@ -1178,14 +1300,17 @@ ErasureConsensus::Gathered ErasureConsensus::collect(const Address& a, bool para
   return g;
 }
 
+const uint8_t* ErasureConsensus::Gathered::payload(size_t s) const {
+  const auto& sh = shards[s];
+  return sh.first < h.k ? block.data() + (size_t)sh.first * h.shard_size : sh.second.data() + ShardHeader::kSize;
+}
+
 std::unique_ptr<Block> ErasureConsensus::assemble(const Address& a, Gathered& g,
                                                   const uint8_t* rebuilt, size_t stride) {
   const int k = o_.k;
   const size_t S = g.h.shard_size;
-  Buffer block((size_t)k * S);
-  for (auto& s : g.shards)
-    if (s.first < k)
-      std::memcpy(block.data() + (size_t)s.first * S, s.second.data() + ShardHeader::kSize, S);
+  Buffer block = std::move(g.block);  // the data shards in hand are in place
+  block.resize((size_t)k * S);
   for (size_t r = 0; r < g.lost.size(); ++r)
     std::memcpy(block.data() + (size_t)g.lost[r] * S, rebuilt + r * stride, S);
   block.resize(g.h.block_size);
@@ -1200,8 +1325,8 @@ std::unique_ptr<Block> ErasureConsensus::assemble(const Address& a, Gathered& g,
   return b;
 }
 
-std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
-  if (a.mutable_block()) return backend_->fetch(a);
+std::unique_ptr<Block> ErasureConsensus::_fetch(Address a, std::optional<int> local_version) {
+  if (a.mutable_block()) return backend_->fetch(a, local_version);
   const int k = o_.k;
   Gathered g = collect(a, true);
   if (g.err) std::rethrow_exception(g.err);
@@ -1213,7 +1338,7 @@ std::unique_ptr<Block> ErasureConsensus::_fetch(const Address& a) {
     Buffer surv((size_t)k * S);
     for (int s = 0; s < k; ++s) {
       sidx[s] = (uint8_t)g.shards[s].first;
-      std::memcpy(surv.data() + (size_t)s * S, g.shards[s].second.data() + ShardHeader::kSize, S);
+      std::memcpy(surv.data() + (size_t)s * S, g.payload(s), S);
     }
     out.resize(g.lost.size() * S);
     codec_.rebuild(k, o_.m, S, 1, sidx.data(), surv.data(), g.lost.data(), (int)g.lost.size(),
@@ -1355,9 +1480,11 @@ std::unique_ptr<Block> ErasureConsensus::recover(const Address& a, bool parallel
 // then reassembly + CHB check on the pool; `res` is called in request
 // order.  The reference hands the whole batch over at once too
 // (Consensus::_fetch(vector<AddressVersion>), Consensus.cc:101-124).
-void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
+void ErasureConsensus::_fetch(const std::vector<AddressVersion>& request, ReceiveBlock res) {
   const int k = o_.k, m = o_.m;
-  const size_t n = addresses.size();
+  const size_t n = request.size();
+  std::vector<Address> addresses(n);
+  for (size_t i = 0; i < n; ++i) addresses[i] = request[i].first;
   std::vector<std::unique_ptr<Block>> blocks(n);
   std::vector<std::exception_ptr> errs(n);
   std::vector<size_t> imm;
@@ -1367,7 +1494,7 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       continue;
     }
     try {
-      blocks[i] = backend_->fetch(addresses[i]);
+      blocks[i] = backend_->fetch(addresses[i], request[i].second);
     } catch (Error&) {
       errs[i] = std::current_exception();
     }
@@ -1497,7 +1624,7 @@ void ErasureConsensus::_fetch(const std::vector<Address>& addresses, const Recei
       Gathered& x = g[fb.grp->ids[fb.b0 + bi]];
       for (int s = 0; s < k; ++s) {
         uint8_t* slot = fb.surv + (bi * k + s) * fb.S;
-        std::memcpy(slot, x.shards[s].second.data() + ShardHeader::kSize, x.h.shard_size);
+        std::memcpy(slot, x.payload(s), x.h.shard_size);
         std::memset(slot + x.h.shard_size, 0, fb.S - x.h.shard_size);
         if (!fb.grp->uniform) fb.sidx[bi * k + s] = (uint8_t)x.shards[s].first;
       }
@@ -1544,8 +1671,8 @@ void ErasureConsensus::_resign() { backend_->resign(); }
 // MissingBlock when no holder removed anything.  A CHB's removal never
 // conflicts (its validation has no conflict outcome), so the reference's
 // re-sign-and-retry loop on Conflict has nothing to retry here.
-void ErasureConsensus::_remove(const Address& a, const RemoveSignature& rs) {
-  if (a.mutable_block()) return backend_->remove(a, rs);
+void ErasureConsensus::_remove(Address a, RemoveSignature rs) {
+  if (a.mutable_block()) return backend_->remove(a, std::move(rs));
   const int total = o_.k + o_.m;
   const ShardKeys keys(a);
   // (node, shard index; -1: every index) pairs to visit: the placement

@@ -144,6 +144,11 @@ class PinnedArena {
   size_t keep_;
 };
 
+// Shards of at most kFrameShardMax wire bytes are framed by the store in
+// runs sharing one buffer of up to kFrameRunBytes (ErasureConsensus::place_batch).
+constexpr size_t kFrameShardMax = (size_t)16 << 10;
+constexpr size_t kFrameRunBytes = (size_t)256 << 10;
+
 // Default shard bytes one store_many, fetch or repair chunk stages (pinned)
 // and hands to one codec call at most (ErasureOptions::stage_bytes).
 constexpr size_t kStageBytes = (size_t)512 << 20;
@@ -185,9 +190,14 @@ Buffer encode_shard(const ShardHeader& h, const uint8_t* payload);
 // encode_shard with `index` in place of h.index (one header per block shared
 // by the threads framing its shards).
 Buffer encode_shard(const ShardHeader& h, const uint8_t* payload, int index);
+// encode_shard into kSize + h.shard_size bytes at w (a slot of a buffer that
+// frames many shards).
+void frame_shard(const ShardHeader& h, const uint8_t* payload, int index, uint8_t* w);
 // Parses and validates (magic, version, geometry, S = memo_ec_shard_size(B,k),
 // payload length, CRC32C over header and payload); throws ValidationFailed.
 ShardHeader decode_shard(const Buffer& wire, const uint8_t** payload);
+// decode_shard of the n bytes at w (a silo's view of a stored shard).
+ShardHeader decode_shard_view(const uint8_t* w, size_t n, const uint8_t** payload);
 // *payload would point into a temporary that dies with the call.
 ShardHeader decode_shard(Buffer&& wire, const uint8_t** payload) = delete;
 // The header alone (the first kSize bytes): magic, version and geometry are
@@ -204,6 +214,10 @@ struct ShardKeys {
 };
 // Silo key of shard `index` of block `address` (ShardKeys(address)(index)).
 Key shard_key(const Address& address, int index);
+// The peer of a node in a network built before its consensus (tests,
+// benches): a ShardLocal in front of make_replica_local(storage), what
+// ErasureConsensus::make_local makes over a ReplicationConsensus backend.
+std::unique_ptr<Local> make_shard_local(std::unique_ptr<Silo> storage);
 uint32_t crc32c(const uint8_t* p, size_t n, uint32_t crc = 0);
 
 // ------------------------------------------------------------ thread pool
@@ -298,13 +312,38 @@ struct ErasureOptions {
   int verify_subsets = 64;
 };
 
+// The peer ErasureConsensus::make_local makes, in front of its backend's
+// peer: a shard (the "MECS" framing) must pass its header checks and
+// CRC32C and sit under its own key (shard_key(address, index)) -- the shard
+// validation that replaces LocalPeer::store's CHB re-hash (Paxos.cc:1571-
+// 1575) -- and may only replace a shard; any other value is the backend
+// peer's to validate (the mutable blocks' replicas).
+class ShardLocal : public Local {
+ public:
+  explicit ShardLocal(std::unique_ptr<Local> backend);
+  void validate(const Key& k, const uint8_t* v, size_t n) const override;
+
+ private:
+  std::unique_ptr<Local> backend_;
+};
+
 class ErasureConsensus : public StackedConsensus {
  public:
   ErasureConsensus(std::unique_ptr<Consensus> backend, Overlay& overlay, ErasureOptions o);
   ~ErasureConsensus() override;
 
-  std::string redundancy() const override;
-  std::string stats() const override;
+  // {"type":"erasure","k","m","desired_factor"}
+  std::string redundancy() override;
+  std::string stats() override;
+  std::string stats_text() const;  // stats() for const callers
+  // Where a block's shards are, as this client's placement index records
+  // them (Consensus::stat, Consensus.hh:85-95; Paxos's PaxosStat lists the
+  // quorum): {"placed", "k", "m", "block_size", "holders" (hex, "" for an
+  // unplaced shard), "reachable"}.
+  std::unique_ptr<Stat> stat(const Address& address) override;
+  // A ShardLocal in front of the backend's peer (Consensus.hh:100-105).
+  std::unique_ptr<Local> make_local(std::optional<int> port, std::optional<IpAddress> listen_address,
+                                    std::unique_ptr<Silo> storage) override;
 
   struct RepairReport {
     size_t blocks_checked = 0, blocks_repaired = 0, shards_rebuilt = 0;
@@ -342,7 +381,8 @@ class ErasureConsensus : public StackedConsensus {
   size_t node_blocks(const Address& node) const;
   // Evictions scheduled and not yet run.
   size_t pending_evictions() const;
-  // Store many immutable blocks with one encode call per batch.
+  // Store many immutable blocks with one encode call per batch (mutable ones
+  // go to the backend one by one).
   void store_many(const std::vector<Block>& blocks);
   const Codec& codec() const { return codec_; }
   uint64_t arena_leases() const { return arena_.leases(); }
@@ -356,12 +396,18 @@ class ErasureConsensus : public StackedConsensus {
   size_t pending_removes() const;
 
  protected:
-  void _store(const Block& b, StoreMode mode) override;
-  std::unique_ptr<Block> _fetch(const Address& a) override;
-  void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) override;
+  // Immutable blocks: encoded and placed (the resolver has nothing to
+  // resolve: a CHB store never conflicts); mutable: the backend, resolver
+  // and all.
+  void _store(std::unique_ptr<Block> block, StoreMode mode,
+              std::unique_ptr<ConflictResolver> resolver) override;
+  // local_version: a mutable block's, passed to the backend (a CHB has no
+  // version).
+  std::unique_ptr<Block> _fetch(Address address, std::optional<int> local_version) override;
+  void _fetch(const std::vector<AddressVersion>& addresses, ReceiveBlock res) override;
   // Consensus::remove (Consensus.cc:135-240) with CHB removal semantics
   // (CHB::_validate_remove, CHB.cc:203-259): see erasure_consensus.cc.
-  void _remove(const Address& a, const RemoveSignature& rs) override;
+  void _remove(Address address, RemoveSignature rs) override;
   // Leaving the network: the mutable blocks' backend hands its blocks off
   // (Paxos::_resign, Paxos.cc:2091-2131, which rebalances mutable blocks
   // only); shards stay where they are, and the remaining nodes' eviction
@@ -381,6 +427,7 @@ class ErasureConsensus : public StackedConsensus {
     Placement pl;
     bool set = false;
   };
+  void store_one(const Block& b);
   struct EncodeJob {
     const Block* block;
     std::promise<Buffer> parity;  // m x S
@@ -388,9 +435,13 @@ class ErasureConsensus : public StackedConsensus {
   // A block's shards in hand for a fetch, and its missing data shards.
   struct Gathered {
     ShardHeader h;
-    std::vector<std::pair<int, Buffer>> shards;  // the k used, sorted by index
-    std::vector<uint8_t> lost;                   // data-shard indices to rebuild
+    // the k used, sorted by index: data shards' payloads in `block`, parity
+    // shards' wire bytes in the entry
+    std::vector<std::pair<int, Buffer>> shards;
+    Buffer block;               // k x S: the data shards in hand in their slots
+    std::vector<uint8_t> lost;  // data-shard indices to rebuild
     std::exception_ptr err;
+    const uint8_t* payload(size_t s) const;  // shards[s]'s S payload bytes
   };
   Gathered collect(const Address& a, bool parallel);
   // The block from g's data shards and, for g.lost[r], the S bytes at
@@ -413,9 +464,11 @@ class ErasureConsensus : public StackedConsensus {
                                  const uint8_t* parity, size_t S, std::vector<Placed>& placed);
   void batcher_loop();
   // from (k + m entries): the node each gathered shard came from
+  // block: data shards' payloads straight into it (see the definition)
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true,
-                                                    std::vector<Node*>* from = nullptr);
+                                                    std::vector<Node*>* from = nullptr,
+                                                    Buffer* block = nullptr);
   // A block whose reassembly failed its address, from another k-subset of
   // its reachable shards; the disagreeing shards rewritten (AddressMismatch
   // when no subset within verify_subsets matches).
@@ -464,7 +517,9 @@ class ErasureConsensus : public StackedConsensus {
   bool mstop_ = false;
   int sub_token_ = -1;
   std::thread mthread_;
-  std::atomic<uint64_t> stored_{0}, fetched_{0}, decoded_{0}, repaired_{0}, evictions_{0};
+  // fetched_ and decoded_ are added to per block by every pool thread
+  Counter stored_, fetched_, decoded_;
+  std::atomic<uint64_t> repaired_{0}, evictions_{0};
   // reassemblies that failed their address and were recovered from another
   // k-subset; shards found wrong that way and rewritten
   std::atomic<uint64_t> subset_recoveries_{0}, corrupt_rewritten_{0};
@@ -478,13 +533,11 @@ class ErasureConsensus : public StackedConsensus {
   };
   std::map<Address, std::vector<OwedRemove>> pending_rm_;  // node -> removals still owed
   // in-flight fetches from this client per node (the reference's
-  // Paxos::_transfers), hashed into padded slots
-  struct alignas(64) TransferSlot {
-    std::atomic<int> n{0};
-  };
-  mutable std::array<TransferSlot, 64> transfers_;
-  std::atomic<int>& transfers(const Node* nd) const {
-    return transfers_[(reinterpret_cast<uintptr_t>(nd) >> 6) % transfers_.size()].n;
+  // Paxos::_transfers), hashed into per-thread-slot counters: every shard
+  // fetch adds and subtracts, only a degraded fetch's ordering reads them
+  mutable std::array<Counter, 64> transfers_;
+  Counter& transfers(const Node* nd) const {
+    return transfers_[(reinterpret_cast<uintptr_t>(nd) >> 6) % transfers_.size()];
   }
 };
 

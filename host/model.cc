@@ -212,27 +212,57 @@ bool chb_valid(const Address& address, const Buffer& salt, const Address& owner,
   return std::memcmp(want.value.data(), address.value.data(), 31) == 0;
 }
 
+// ------------------------------------------------------------- counters
+size_t Counter::slot() {
+  static std::atomic<size_t> next{0};
+  thread_local const size_t s = next.fetch_add(1, std::memory_order_relaxed) % kSlots;
+  return s;
+}
+
 // ---------------------------------------------------------------- silo
-int Silo::set(const Key& k, const Buffer& v, bool insert, bool update) {
-  if (capacity_ >= 0 && usage_ + (int64_t)v.size() > capacity_)
+void Silo::check_space(size_t n) const {
+  if (capacity_ >= 0 && usage_.load() + (int64_t)n > capacity_)
     throw silo::InsufficientSpace("insufficient space");
+}
+
+int Silo::set(const Key& k, const Buffer& v, bool insert, bool update) {
+  check_space(v.size());
   const int delta = _set(k, v, insert, update);
   usage_ += delta;
   return delta;
 }
 
 int Silo::set(const Key& k, Buffer&& v, bool insert, bool update) {
-  if (capacity_ >= 0 && usage_ + (int64_t)v.size() > capacity_)
-    throw silo::InsufficientSpace("insufficient space");
+  check_space(v.size());
   const int delta = _set_moved(k, std::move(v), insert, update);
   usage_ += delta;
   return delta;
+}
+
+int Silo::set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,
+                     bool update) {
+  check_space(n);
+  const int delta = _set_shared(k, std::move(bytes), n, insert, update);
+  usage_ += delta;
+  return delta;
+}
+
+int Silo::_set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,
+                      bool update) {
+  return _set_moved(k, Buffer(bytes.get(), bytes.get() + n), insert, update);
 }
 
 int Silo::erase(const Key& k) {
   const int delta = _erase(k);
   usage_ += delta;
   return delta;
+}
+
+bool Silo::_read(const Key& k, const ReadSink& sink) const {
+  Buffer v;
+  if (!_try_get(k, v)) return false;
+  sink(v.data(), v.size());
+  return true;
 }
 
 bool Silo::_try_get(const Key& k, Buffer& out) const {
@@ -261,42 +291,66 @@ bool MemorySilo::_contains(const Key& k) const {
   return st.blocks.count(k) != 0;
 }
 
+MemorySilo::Value MemorySilo::find(const Key& k) const {
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  auto it = st.blocks.find(k);
+  return it == st.blocks.end() ? Value() : it->second;
+}
+
 bool MemorySilo::_try_get(const Key& k, Buffer& out) const {
-  std::shared_ptr<const Buffer> v;
-  {
-    Stripe& st = stripe(k);
-    std::lock_guard<std::mutex> g(st.mu);
-    auto it = st.blocks.find(k);
-    if (it == st.blocks.end()) return false;
-    v = it->second;
-  }
-  out = *v;
+  const Value v = find(k);
+  if (!v.p) return false;
+  out.assign(v.p.get(), v.p.get() + v.n);
+  return true;
+}
+
+bool MemorySilo::_try_get_prefix(const Key& k, size_t n, Buffer& out) const {
+  const Value v = find(k);
+  if (!v.p) return false;
+  out.assign(v.p.get(), v.p.get() + std::min(n, v.n));
+  return true;
+}
+
+bool MemorySilo::_read(const Key& k, const ReadSink& sink) const {
+  const Value v = find(k);  // the reference keeps the bytes alive outside the lock
+  if (!v.p) return false;
+  sink(v.p.get(), v.n);
   return true;
 }
 
 Buffer MemorySilo::_get(const Key& k) const {
-  std::shared_ptr<const Buffer> v;
-  {
-    Stripe& st = stripe(k);
-    std::lock_guard<std::mutex> g(st.mu);
-    auto it = st.blocks.find(k);
-    if (it == st.blocks.end()) throw silo::MissingKey("missing key " + k.hex());
-    v = it->second;
-  }
-  return *v;
+  const Value v = find(k);
+  if (!v.p) throw silo::MissingKey("missing key " + k.hex());
+  return Buffer(v.p.get(), v.p.get() + v.n);
 }
 
+namespace {
+// The bytes of a whole buffer, sharing its ownership (aliasing constructor).
+std::shared_ptr<const uint8_t> bytes_of(std::shared_ptr<const Buffer> b) {
+  const uint8_t* p = b->data();
+  return std::shared_ptr<const uint8_t>(std::move(b), p);
+}
+}  // namespace
+
 int MemorySilo::_set(const Key& k, const Buffer& v, bool insert, bool update) {
-  return put(k, std::make_shared<const Buffer>(v), insert, update);  // the copy, outside the lock
+  // the copy, outside the lock
+  return put(k, Value{bytes_of(std::make_shared<const Buffer>(v)), v.size()}, insert, update);
 }
 
 int MemorySilo::_set_moved(const Key& k, Buffer&& v, bool insert, bool update) {
-  return put(k, std::make_shared<const Buffer>(std::move(v)), insert, update);
+  const size_t n = v.size();
+  return put(k, Value{bytes_of(std::make_shared<const Buffer>(std::move(v))), n}, insert, update);
 }
 
-int MemorySilo::put(const Key& k, std::shared_ptr<const Buffer> nv, bool insert, bool update) {
-  std::shared_ptr<const Buffer> old;  // freed outside the lock
-  const int size = (int)nv->size();
+int MemorySilo::_set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,
+                            bool update) {
+  return put(k, Value{std::move(bytes), n}, insert, update);
+}
+
+int MemorySilo::put(const Key& k, Value nv, bool insert, bool update) {
+  Value old;  // freed outside the lock
+  const int size = (int)nv.n;
   Stripe& st = stripe(k);
   std::lock_guard<std::mutex> g(st.mu);
   auto it = st.blocks.find(k);
@@ -306,19 +360,19 @@ int MemorySilo::put(const Key& k, std::shared_ptr<const Buffer> nv, bool insert,
     return size;
   }
   if (!update) throw silo::Collision("key exists " + k.hex());
-  const int delta = size - (int)it->second->size();
+  const int delta = size - (int)it->second.n;
   old = std::move(it->second);
   it->second = std::move(nv);
   return delta;
 }
 
 int MemorySilo::_erase(const Key& k) {
-  std::shared_ptr<const Buffer> old;
+  Value old;
   Stripe& st = stripe(k);
   std::lock_guard<std::mutex> g(st.mu);
   auto it = st.blocks.find(k);
   if (it == st.blocks.end()) throw silo::MissingKey("missing key " + k.hex());
-  const int delta = -(int)it->second->size();
+  const int delta = -(int)it->second.n;
   old = std::move(it->second);
   st.blocks.erase(it);
   return delta;
@@ -372,7 +426,7 @@ FilesystemSilo::FilesystemSilo(std::string root, int64_t capacity)
         Key k;
         if (f.is_regular_file() && key_of(f.path().filename().string(), k)) used += (int64_t)f.file_size();
       }
-  usage_ = used;
+  usage_ += used;
 }
 
 std::string FilesystemSilo::path(const Key& k, bool make_dir) const {
@@ -457,6 +511,7 @@ std::vector<Key> FilesystemSilo::_list() {
 void Node::store(const Key& k, const Buffer& v) {
   if (!up || evicted) throw Unavailable("node down");
   if (fail_stores) throw Unavailable("store refused");
+  local->validate(k, v.data(), v.size());
   silo->set(k, v, true, true);
   ++stores;
 }
@@ -464,13 +519,28 @@ void Node::store(const Key& k, const Buffer& v) {
 void Node::store(const Key& k, Buffer&& v) {
   if (!up || evicted) throw Unavailable("node down");
   if (fail_stores) throw Unavailable("store refused");
+  local->validate(k, v.data(), v.size());
   silo->set(k, std::move(v), true, true);
   ++stores;
 }
 
+void Node::store_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n) {
+  if (!up || evicted) throw Unavailable("node down");
+  if (fail_stores) throw Unavailable("store refused");
+  local->validate(k, bytes.get(), n);
+  silo->set_shared(k, std::move(bytes), n, true, true);
+  ++stores;
+}
+
+bool Node::try_read(const Key& k, const ReadSink& sink) const {
+  if (!up || evicted) throw Unavailable("node down");
+  fetches++;
+  return silo->read(k, sink);
+}
+
 Buffer Node::fetch(const Key& k) const {
   if (!up || evicted) throw Unavailable("node down");
-  const_cast<Node*>(this)->fetches++;
+  fetches++;
   return silo->get(k);
 }
 
@@ -481,7 +551,7 @@ void Node::remove(const Key& k) {
 
 bool Node::try_fetch(const Key& k, Buffer& out) const {
   if (!up || evicted) throw Unavailable("node down");
-  const_cast<Node*>(this)->fetches++;
+  fetches++;
   return silo->try_get(k, out);
 }
 
@@ -505,10 +575,23 @@ Overlay::Overlay() {
 
 Overlay::~Overlay() = default;
 
+// ----------------------------------------------------------------- peers
+Local::Local(std::unique_ptr<Silo> storage, std::optional<int> port, std::optional<IpAddress> listen)
+    : storage_(std::move(storage)), port_(port.value_or(0)), listen_(std::move(listen)) {
+  if (!storage_) throw Error("local: no storage");
+}
+
+void Local::validate(const Key&, const uint8_t*, size_t) const {}
+
 std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Silo> silo) {
+  return add_node(id, std::make_unique<Local>(std::move(silo)));
+}
+
+std::shared_ptr<Node> Overlay::add_node(const Address& id, std::unique_ptr<Local> local) {
   auto n = std::make_shared<Node>();
   n->id = id;
-  n->silo = std::move(silo);
+  n->silo = &local->storage();
+  n->local = std::move(local);
   {
     std::lock_guard<std::mutex> g(mu_);
     auto next = std::make_unique<Snapshot>(*snap());
@@ -606,18 +689,33 @@ std::vector<std::shared_ptr<Node>> Overlay::lookup(const Address& address, int n
 }
 
 // ------------------------------------------------------------- consensus
-void Consensus::_fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
+void Consensus::_fetch(const std::vector<AddressVersion>& addresses, ReceiveBlock res) {
   for (auto& a : addresses) {
     std::unique_ptr<Block> b;
     try {
-      b = fetch(a);
+      b = fetch(a.first, a.second);
     } catch (Error&) {
-      res(a, nullptr, std::current_exception());
+      res(a.first, nullptr, std::current_exception());
       continue;
     }
-    res(a, std::move(b), nullptr);
+    res(a.first, std::move(b), nullptr);
   }
 }
+
+std::unique_ptr<Consensus::Stat> Consensus::stat(const Address&) { return std::make_unique<Stat>(); }
+
+std::unique_ptr<Local> Consensus::make_local(std::optional<int> port, std::optional<IpAddress> listen_address,
+                                             std::unique_ptr<Silo> storage) {
+  return std::make_unique<Local>(std::move(storage), port, std::move(listen_address));
+}
+
+std::shared_ptr<Remote> Consensus::make_remote(std::shared_ptr<DockConnection> connection) {
+  return std::make_shared<Remote>(std::move(connection));
+}
+
+std::string Consensus::redundancy() { return to_json({{"desired_factor", "1.0"}, {"type", "none"}}); }
+
+std::string Consensus::stats() { return to_json({{"type", "none"}}); }
 
 // ----------------------------------------------------------- replication
 namespace {
@@ -635,61 +733,160 @@ Buffer encode_replica(const Block& b) {
   return out;
 }
 
-Block decode_replica(const Address& a, const Buffer& r) {
-  if (r.size() < 40) throw ValidationFailed("short replica");
-  uint32_t v, sl;
-  std::memcpy(&v, r.data(), 4);
-  std::memcpy(&sl, r.data() + 4, 4);
-  if (40 + (size_t)sl > r.size()) throw ValidationFailed("bad replica");
+// The fields of a replica value without copying its data.
+struct ReplicaView {
+  uint32_t version;
+  Address owner;
+  const uint8_t* salt;
+  uint32_t salt_len;
+  const uint8_t* data;
+  size_t data_len;
+};
+ReplicaView view_replica(const uint8_t* r, size_t n) {
+  if (n < 40) throw ValidationFailed("short replica");
+  ReplicaView v;
+  std::memcpy(&v.version, r, 4);
+  std::memcpy(&v.salt_len, r + 4, 4);
+  if (40 + (size_t)v.salt_len > n) throw ValidationFailed("bad replica");
+  v.owner = Address(r + 8, 0, false);
+  v.salt = r + 40;
+  v.data = r + 40 + v.salt_len;
+  v.data_len = n - 40 - v.salt_len;
+  return v;
+}
+
+Block decode_replica(const Address& a, const uint8_t* r, size_t n) {
+  const ReplicaView v = view_replica(r, n);
   Block b;
   b.address = a;
-  b.version = (int)v;
+  b.version = (int)v.version;
   b.is_mutable = a.mutable_block();
-  b.owner = Address(r.data() + 8, 0, false);
-  b.salt.assign(r.begin() + 40, r.begin() + 40 + sl);
-  b.data.assign(r.begin() + 40 + sl, r.end());
+  b.owner = v.owner;
+  b.salt.assign(v.salt, v.salt + v.salt_len);
+  b.data.assign(v.data, v.data + v.data_len);
   return b;
 }
+
+// Paxos::LocalPeer restated for the replication path: what it stores is
+// validated as LocalPeer::store does (Paxos.cc:1568-1615).
+class ReplicaLocal : public Local {
+ public:
+  using Local::Local;
+  void validate(const Key& k, const uint8_t* v, size_t n) const override {
+    validate_replica(k, v, n);
+    // validate with the previous version, if any
+    bool stored_mutable = false;
+    uint32_t stored_version = 0;
+    std::unique_ptr<Block> current;
+    const uint32_t version = view_replica(v, n).version;
+    auto prev = [&](const uint8_t* p, size_t pn) {
+      const ReplicaView pv = view_replica(p, pn);
+      stored_mutable = k.mutable_block();
+      stored_version = pv.version;
+      if (stored_mutable && pv.version >= version)
+        current = std::make_unique<Block>(decode_replica(k, p, pn));
+    };
+    if (!storage().read(k, prev)) return;
+    if (current)
+      throw Conflict("stored version " + std::to_string(stored_version) + " is not older than " +
+                         std::to_string(version),
+                     std::move(current));
+  }
+};
 }  // namespace
 
-std::string ReplicationConsensus::redundancy() const {
+void validate_replica(const Key& k, const uint8_t* v, size_t n) {
+  const ReplicaView r = view_replica(v, n);
+  if (k.mutable_block()) return;  // a mutable block's own signature checks are outside this path
+  // CHB::_validate (CHB.cc:79-99): the content hashes to the address
+  Buffer saltowner(r.salt, r.salt + r.salt_len);
+  if (r.owner) saltowner.insert(saltowner.end(), r.owner.value.begin(), r.owner.value.end());
+  const auto h = sha256(saltowner.data(), saltowner.size(), r.data, r.data_len);
+  if (std::memcmp(h.data(), k.value.data(), 31) != 0) throw ValidationFailed("CHB address mismatch");
+}
+
+std::string ReplicationConsensus::redundancy() {
   return to_json({{"type", "replication"}, {"desired_factor", std::to_string(factor_)}});
 }
 
-void ReplicationConsensus::_store(const Block& b, StoreMode mode) {
-  auto owners = mode == STORE_INSERT ? overlay_.allocate(b.address, factor_)
-                                     : overlay_.lookup(b.address, factor_);
-  if (owners.empty()) throw TooFewPeers("no storage peer");
-  const Buffer rep = encode_replica(b);
-  int reached = 0;
-  for (auto& o : owners) {
-    try {
-      o->store(replica_key(b.address), rep);
-      ++reached;
-    } catch (Unavailable&) {
-    }
-  }
-  if (reached == 0) throw TooFewPeers("no owner reachable");
+std::string ReplicationConsensus::stats() {
+  return to_json({{"type", "replication"}, {"factor", std::to_string(factor_)}});
 }
 
-std::unique_ptr<Block> ReplicationConsensus::_fetch(const Address& a) {
+std::unique_ptr<Local> ReplicationConsensus::make_local(std::optional<int> port,
+                                                        std::optional<IpAddress> listen_address,
+                                                        std::unique_ptr<Silo> storage) {
+  return std::make_unique<ReplicaLocal>(std::move(storage), port, std::move(listen_address));
+}
+
+std::unique_ptr<Local> make_replica_local(std::unique_ptr<Silo> storage) {
+  return std::make_unique<ReplicaLocal>(std::move(storage));
+}
+
+void ReplicationConsensus::_store(std::unique_ptr<Block> block, StoreMode mode,
+                                  std::unique_ptr<ConflictResolver> resolver) {
+  std::unique_ptr<Block> resolved;  // the resolver's block, once there is one
+  for (;;) {
+    const Block& b = resolved ? *resolved : *block;
+    auto owners = mode == STORE_INSERT ? overlay_.allocate(b.address, factor_)
+                                       : overlay_.lookup(b.address, factor_);
+    if (owners.empty()) throw TooFewPeers("no storage peer");
+    const Buffer rep = encode_replica(b);
+    int reached = 0;
+    try {
+      for (auto& o : owners) {
+        try {
+          o->store(replica_key(b.address), rep);
+          ++reached;
+        } catch (Unavailable&) {
+        }
+      }
+    } catch (Conflict& c) {
+      // Consensus::_store (Consensus.cc:59-91): the resolver's block, or
+      // the conflict to the caller
+      if (!resolver || !c.current) throw;
+      Block failed = b;
+      auto nb = (*resolver)(failed, *c.current);
+      if (!nb) throw;
+      resolved = std::move(nb);
+      mode = STORE_UPDATE;
+      continue;
+    }
+    if (reached == 0) throw TooFewPeers("no owner reachable");
+    return;
+  }
+}
+
+std::unique_ptr<Block> ReplicationConsensus::_fetch(Address a, std::optional<int> local_version) {
   bool any_up = false;
   for (auto& o : overlay_.lookup(a, factor_)) {
     try {
-      auto r = o->fetch(replica_key(a));
-      auto b = std::make_unique<Block>(decode_replica(a, r));
-      if (!b->is_mutable && !chb_valid(a, b->salt, b->owner, b->data)) continue;
+      std::unique_ptr<Block> b;
+      bool bad = false;
+      auto take = [&](const uint8_t* r, size_t n) {
+        try {
+          b = std::make_unique<Block>(decode_replica(a, r, n));
+        } catch (ValidationFailed&) {
+          bad = true;
+        }
+      };
+      if (!o->try_read(replica_key(a), take)) {
+        any_up = true;
+        continue;
+      }
+      if (bad || (!b->is_mutable && !chb_valid(a, b->salt, b->owner, b->data))) continue;
+      // no newer than the caller's copy: nothing to return (Paxos::_fetch
+      // with a local version)
+      if (b->is_mutable && local_version && b->version <= *local_version) return nullptr;
       return b;
     } catch (Unavailable&) {
-    } catch (silo::MissingKey&) {
-      any_up = true;
     }
   }
   if (!any_up) throw TooFewPeers("no replica reachable");
   throw MissingBlock("missing block " + a.hex());
 }
 
-void ReplicationConsensus::_remove(const Address& a, const RemoveSignature&) {
+void ReplicationConsensus::_remove(Address a, RemoveSignature) {
   int count = 0;
   for (auto& o : overlay_.lookup(a, factor_)) {
     try {

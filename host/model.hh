@@ -205,10 +205,50 @@ RemoveSignature chb_sign_remove_group(const Address& chb, const Buffer& group_ke
 std::string chb_validate_remove(const Address& chb, const Address& owner,
                                 const RemoveSignature& rs, const OwnerDirectory* dir);
 
+// --------------------------------------------------------------- counters
+// A counter that many threads add to: per-thread-slot atomics on lines of
+// their own, summed by load().  One shared atomic line that every store or
+// fetch thread writes moves between cores on each add, which on a many-core
+// host costs more than the silo operation it counts.
+class Counter {
+ public:
+  void add(int64_t d) { s_[slot()].v.fetch_add(d, std::memory_order_relaxed); }
+  void operator++() { add(1); }
+  void operator++(int) { add(1); }
+  void operator+=(int64_t d) { add(d); }
+  int64_t load() const {
+    int64_t t = 0;
+    for (auto& x : s_) t += x.v.load(std::memory_order_relaxed);
+    return t;
+  }
+  operator int64_t() const { return load(); }
+
+ private:
+  static constexpr size_t kSlots = 16;
+  static size_t slot();  // the calling thread's slot (assigned round robin)
+  struct alignas(64) Slot {
+    std::atomic<int64_t> v{0};
+  };
+  std::array<Slot, kSlots> s_;
+};
+
 // ------------------------------------------------------------------- silo
 // silo::Silo (src/memo/silo/Silo.hh:33-129): get/set/erase/list with the
 // MissingKey / Collision contract; subclasses implement _get/_set/_erase/_list.
 using Key = Address;
+
+// A non-owning callable (bytes, size) for Silo::read: no allocation per call.
+class ReadSink {
+ public:
+  template <class F>
+  ReadSink(F& f)  // NOLINT: implicit from any callable lvalue
+      : obj_(&f), call_([](void* o, const uint8_t* p, size_t n) { (*static_cast<F*>(o))(p, n); }) {}
+  void operator()(const uint8_t* p, size_t n) const { call_(obj_, p, n); }
+
+ private:
+  void* obj_;
+  void (*call_)(void*, const uint8_t*, size_t);
+};
 
 class Silo {
  public:
@@ -221,14 +261,23 @@ class Silo {
   // absent.  Index rescans read shard headers only.
   bool try_get_prefix(const Key& k, size_t n, Buffer& out) const { return _try_get_prefix(k, n, out); }
   bool contains(const Key& k) const { return _contains(k); }
+  // The value handed to sink(bytes, size) -- a view valid during the call --
+  // instead of copied out; false when absent.  The fetch paths validate a
+  // shard and copy its payload into place in one pass.
+  bool read(const Key& k, const ReadSink& sink) const { return _read(k, sink); }
   // insert: accept a new key; update: accept an existing key.
   int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
   // set() of a value the caller gives up (a silo may keep it without a copy)
   int set(const Key& k, Buffer&& v, bool insert = true, bool update = false);
+  // set() of the n bytes at `bytes`, which may share their allocation with
+  // other keys' values (a batch of shards framed into one buffer); a silo
+  // may keep the reference instead of a copy
+  int set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert = true,
+                 bool update = false);
   int erase(const Key& k);
   std::vector<Key> list() { return _list(); }
   virtual std::string type() const = 0;
-  int64_t usage() const { return usage_; }
+  int64_t usage() const { return usage_.load(); }
   int64_t capacity() const { return capacity_; }
 
  protected:
@@ -236,12 +285,17 @@ class Silo {
   virtual bool _try_get(const Key& k, Buffer& out) const;  // default: _get + catch
   virtual bool _contains(const Key& k) const;                // default: _try_get
   virtual bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const;  // default: _try_get
+  virtual bool _read(const Key& k, const ReadSink& sink) const;              // default: _try_get
   virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
   virtual int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) { return _set(k, v, insert, update); }
+  // default: a copy through _set_moved
+  virtual int _set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,
+                          bool update);
   virtual int _erase(const Key& k) = 0;
   virtual std::vector<Key> _list() = 0;
+  void check_space(size_t n) const;
   int64_t capacity_;
-  alignas(64) std::atomic<int64_t> usage_{0};  // written by every store thread
+  Counter usage_;  // written by every store thread
 };
 
 // silo::Memory (src/memo/silo/Memory.hh:10-61): the in-memory test silo.
@@ -254,21 +308,32 @@ class MemorySilo : public Silo {
   Buffer _get(const Key& k) const override;
   bool _try_get(const Key& k, Buffer& out) const override;
   bool _contains(const Key& k) const override;
+  bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const override;
+  bool _read(const Key& k, const ReadSink& sink) const override;
   int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
   int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) override;
+  int _set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,
+                  bool update) override;
   int _erase(const Key& k) override;
   std::vector<Key> _list() override;
 
  private:
-  int put(const Key& k, std::shared_ptr<const Buffer> nv, bool insert, bool update);
+  // A stored value: n bytes at p, which may share an allocation with other
+  // keys' values (set_shared; the allocation lives while any of them does).
+  struct Value {
+    std::shared_ptr<const uint8_t> p;
+    size_t n = 0;
+  };
+  Value find(const Key& k) const;  // p null when absent
+  int put(const Key& k, Value nv, bool insert, bool update);
   // Values are immutable once stored: readers take a reference under the
-  // lock and copy outside it, writers copy before taking it.  Hashed, as
-  // the reference's Memory silo (src/memo/silo/Memory.hh:15), in stripes
-  // with a lock each (the reference's silo serves one reactor thread; this
-  // one serves a pool).
+  // lock and copy (or read) outside it, writers copy before taking it.
+  // Hashed, as the reference's Memory silo (src/memo/silo/Memory.hh:15), in
+  // stripes with a lock each (the reference's silo serves one reactor
+  // thread; this one serves a pool).
   struct alignas(64) Stripe {
     mutable std::mutex mu;
-    std::unordered_map<Key, std::shared_ptr<const Buffer>, AddressHash> blocks;
+    std::unordered_map<Key, Value, AddressHash> blocks;
   };
   static constexpr size_t kStripes = 16;
   Stripe& stripe(const Key& k) const { return st_[(AddressHash()(k) >> 56) % kStripes]; }
@@ -301,27 +366,87 @@ class FilesystemSilo : public Silo {
 };
 
 // ------------------------------------------------------------ peers/overlay
+// boost::asio::ip::address stand-in: the textual address a Local listens on.
+struct IpAddress {
+  std::string text;
+};
+
+// doughnut::Local (src/memo/model/doughnut/Local.hh:22-120): the peer that
+// serves a node's silo to the network.  What arrives is validated before the
+// silo keeps it (Local::store, Local.cc:180-215; Paxos::LocalPeer::store
+// re-hashes a CHB, Paxos.cc:1568-1615): validate() is that check, per
+// consensus (Consensus::make_local).  This in-process model opens no port.
+class Local {
+ public:
+  explicit Local(std::unique_ptr<Silo> storage, std::optional<int> port = {},
+                 std::optional<IpAddress> listen_address = {});
+  virtual ~Local() = default;
+  Silo& storage() const { return *storage_; }
+  int port() const { return port_; }
+  const std::optional<IpAddress>& listen_address() const { return listen_; }
+  // The check a value passes before the silo keeps it under key k (the base
+  // peer accepts anything); throws ValidationFailed (or Conflict).
+  virtual void validate(const Key& k, const uint8_t* v, size_t n) const;
+
+ protected:
+  // A peer over another peer's silo (a stacked consensus's Local adds its
+  // checks in front of its backend's: both see one storage).
+  explicit Local(const Local& inner) : storage_(inner.storage_), port_(inner.port_), listen_(inner.listen_) {}
+
+ private:
+  std::shared_ptr<Silo> storage_;
+  int port_;
+  std::optional<IpAddress> listen_;
+};
+
+// Dock::Connection stand-in (src/memo/model/doughnut/Dock.hh): this node's
+// link to another node.
+struct DockConnection {
+  Address peer;
+};
+
+// doughnut::Remote (src/memo/model/doughnut/Remote.hh): a client's handle on
+// another node over a connection (Consensus::make_remote).
+class Remote {
+ public:
+  explicit Remote(std::shared_ptr<DockConnection> connection) : c_(std::move(connection)) {}
+  virtual ~Remote() = default;
+  const Address& id() const { return c_->peer; }
+  const std::shared_ptr<DockConnection>& connection() const { return c_; }
+
+ private:
+  std::shared_ptr<DockConnection> c_;
+};
+
 // A storage node: doughnut::Local with its silo (Local.cc:180-257) as seen
 // through Peer::store/fetch/remove (doughnut/Peer.hh:19-89).  `up` models
-// reachability: a down node raises Unavailable like a failed RPC.
+// reachability: a down node raises Unavailable like a failed RPC.  Stores
+// go through the node's Local: validated, then kept.
 struct Node {
   Address id;
-  std::unique_ptr<Silo> silo;
+  std::unique_ptr<Local> local;
+  Silo* silo = nullptr;  // local->storage()
   std::atomic<bool> up{true};
   std::atomic<bool> evicted{false};
   // store barrier (tests/doughnut.cc:1048-1163 instrumented Local)
   std::atomic<bool> fail_stores{false};
-  // counters written by every store / fetch thread: lines of their own, off
-  // the flags above that every operation reads
-  alignas(64) std::atomic<int64_t> stores{0};
-  alignas(64) std::atomic<int64_t> fetches{0};
+  // counters written by every store / fetch thread (per-thread slots, off
+  // the flags above that every operation reads)
+  Counter stores;
+  mutable Counter fetches;
 
   void store(const Key& k, const Buffer& v);
   void store(const Key& k, Buffer&& v);
+  // store() of n bytes that share an allocation with other values
+  // (Silo::set_shared)
+  void store_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n);
   Buffer fetch(const Key& k) const;
   // fetch() that reports a missing key by returning false (no exception);
   // throws Unavailable when the node is down.
   bool try_fetch(const Key& k, Buffer& out) const;
+  // try_fetch() that hands the value to sink instead of copying it out
+  // (Silo::read)
+  bool try_read(const Key& k, const ReadSink& sink) const;
   // try_fetch() of the value's first n bytes (a shard header).
   bool try_fetch_prefix(const Key& k, size_t n, Buffer& out) const;
   void remove(const Key& k);
@@ -347,7 +472,9 @@ class Overlay {
   // Node::up with the signal (a test may still flip Node::up silently).
   void set_up(const Address& id, bool up);
 
-  // Adds the node and signals its discovery.
+  // Adds the node and signals its discovery: its peer made by a consensus
+  // (Consensus::make_local), or a plain Local over `silo` (no validation).
+  std::shared_ptr<Node> add_node(const Address& id, std::unique_ptr<Local> local);
   std::shared_ptr<Node> add_node(const Address& id, std::unique_ptr<Silo> silo);
   std::shared_ptr<Node> node(const Address& id) const;
   // Every node in rendezvous order for `address` (reachable or not).
@@ -395,8 +522,11 @@ class Overlay {
 };
 
 // -------------------------------------------------------------- consensus
-// consensus::Consensus (src/memo/model/doughnut/Consensus.hh:24-174): the
-// redundancy plugin base.  store/fetch/remove dispatch to the virtuals.
+// consensus::Consensus (src/memo/model/doughnut/Consensus.hh:24-127): the
+// redundancy plugin base.  The public calls dispatch to the protected
+// virtuals; the signatures are the reference's with std::optional for
+// boost::optional, IpAddress / DockConnection for the asio and dock types,
+// and JSON text for elle::json::Json.
 enum StoreMode { STORE_INSERT, STORE_UPDATE };
 
 // Model::ReceiveBlock (src/memo/model/Model.hh:199): called once per
@@ -404,38 +534,89 @@ enum StoreMode { STORE_INSERT, STORE_UPDATE };
 using ReceiveBlock =
     std::function<void(const Address&, std::unique_ptr<Block>, std::exception_ptr)>;
 
+// model::ConflictResolver (src/memo/model/Model.hh:63-87): called when a
+// mutable block's store conflicts with a newer stored version; returns the
+// block to retry with, or null to give up.
+class ConflictResolver {
+ public:
+  virtual ~ConflictResolver() = default;
+  virtual std::unique_ptr<Block> operator()(Block& failed, Block& current) = 0;
+  virtual std::string description() const = 0;
+};
+
+// doughnut::Conflict (src/memo/model/doughnut/Conflict.hh): a store refused
+// because the stored version is as new or newer; carries that version.
+struct Conflict : Error {
+  Conflict(const std::string& what, std::unique_ptr<Block> current)
+      : Error(what), current(std::move(current)) {}
+  std::shared_ptr<Block> current;
+};
+
 class Consensus {
  public:
+  using AddressVersion = std::pair<Address, std::optional<int>>;
   virtual ~Consensus() = default;
-  void store(const Block& b, StoreMode mode = STORE_INSERT) { _store(b, mode); }
-  std::unique_ptr<Block> fetch(const Address& a) { return _fetch(a); }
-  // Consensus::fetch(vector<AddressVersion>, ReceiveBlock) (Consensus.cc:101-106).
-  void fetch(const std::vector<Address>& addresses, const ReceiveBlock& res) {
-    _fetch(addresses, res);
+
+  // Blocks (Consensus.hh:38-61, Consensus.cc:34-141)
+  void store(std::unique_ptr<Block> block, StoreMode mode, std::unique_ptr<ConflictResolver> resolver) {
+    _store(std::move(block), mode, std::move(resolver));
   }
-  // Consensus::remove(Address, RemoveSignature) (Consensus.cc:135-164).
-  void remove(const Address& a, const RemoveSignature& rs = {}) { _remove(a, rs); }
-  // Consensus::resign (Consensus.cc:167-176): the local node is leaving.
+  void fetch(const std::vector<AddressVersion>& addresses, ReceiveBlock res) {
+    _fetch(addresses, std::move(res));
+  }
+  std::unique_ptr<Block> fetch(Address address, std::optional<int> local_version = {}) {
+    return _fetch(address, local_version);
+  }
+  void remove(Address address, RemoveSignature rs) { _remove(address, std::move(rs)); }
   void resign() { _resign(); }
-  // Consensus::redundancy / stats (Consensus.cc:350-357): JSON text.
-  virtual std::string redundancy() const = 0;
-  virtual std::string stats() const { return "{}"; }
+
+  // Stat (Consensus.hh:85-95): what the consensus knows of one block;
+  // Stat::serialize restated as JSON text.
+  class Stat {
+   public:
+    virtual ~Stat() = default;
+    virtual std::string json() const { return "{}"; }
+  };
+  virtual std::unique_ptr<Stat> stat(const Address& address);
+
+  // Factory (Consensus.hh:100-108, Consensus.cc:330-353): the peer serving a
+  // node's silo, and a client's handle on another node.
+  virtual std::unique_ptr<Local> make_local(std::optional<int> port, std::optional<IpAddress> listen_address,
+                                            std::unique_ptr<Silo> storage);
+  virtual std::shared_ptr<Remote> make_remote(std::shared_ptr<DockConnection> connection);
+
+  // Monitoring (Consensus.hh:113-119, Consensus.cc:359-378): JSON text.
+  virtual std::string redundancy();
+  virtual std::string stats();
 
  protected:
-  virtual void _store(const Block& b, StoreMode mode) = 0;
-  virtual std::unique_ptr<Block> _fetch(const Address& a) = 0;
+  virtual void _store(std::unique_ptr<Block> block, StoreMode mode,
+                      std::unique_ptr<ConflictResolver> resolver) = 0;
+  virtual std::unique_ptr<Block> _fetch(Address address, std::optional<int> local_version) = 0;
   // Default: one fetch per address, errors passed to `res`
-  // (Consensus::_fetch, Consensus.cc:108-124).
-  virtual void _fetch(const std::vector<Address>& addresses, const ReceiveBlock& res);
-  virtual void _remove(const Address& a, const RemoveSignature& rs) = 0;
+  // (Consensus::_fetch, Consensus.cc:101-124).
+  virtual void _fetch(const std::vector<AddressVersion>& addresses, ReceiveBlock res);
+  virtual void _remove(Address address, RemoveSignature rs) = 0;
   virtual void _resign() {}  // Consensus::_resign: nothing by default
 };
 
-// consensus::StackedConsensus (Consensus.hh:129-142).
+// consensus::StackedConsensus (Consensus.hh:129-142, Consensus.hxx,
+// Consensus.cc:392-401): a consensus over a backend consensus.
 class StackedConsensus : public Consensus {
  public:
   explicit StackedConsensus(std::unique_ptr<Consensus> backend) : backend_(std::move(backend)) {}
-  Consensus& backend() { return *backend_; }
+  std::shared_ptr<Remote> make_remote(std::shared_ptr<DockConnection> connection) override {
+    return backend_->make_remote(std::move(connection));
+  }
+  // The first consensus of type C down the stack from `top` (itself
+  // included), null if none.
+  template <typename C>
+  static C* find(Consensus* top) {
+    if (auto res = dynamic_cast<C*>(top)) return res;
+    if (auto res = dynamic_cast<StackedConsensus*>(top)) return find<C>(res->backend().get());
+    return nullptr;
+  }
+  const std::unique_ptr<Consensus>& backend() const { return backend_; }
 
  protected:
   std::unique_ptr<Consensus> backend_;
@@ -444,26 +625,46 @@ class StackedConsensus : public Consensus {
 // The replication path memo uses for every block today (Paxos with
 // replication-factor N, immutable branch Paxos.cc:315-391 / 486-519),
 // restated without the Paxos protocol: the full block on `factor` owners,
-// read from the first replica that answers.  The erasure plugin keeps it for
-// mutable (metadata) blocks.
+// read from the first replica that answers.  Its peers validate what they
+// store as Paxos::LocalPeer::store does (Paxos.cc:1568-1615): a CHB replica
+// is re-hashed against its address, and a value already stored under the
+// key is read and checked first (an immutable block over a mutable one is
+// refused; a mutable block's version must grow, else Conflict).  The
+// erasure plugin keeps it for mutable (metadata) blocks.
 class ReplicationConsensus : public Consensus {
  public:
   ReplicationConsensus(Overlay& overlay, int factor) : overlay_(overlay), factor_(factor) {}
-  std::string redundancy() const override;
+  std::string redundancy() override;
+  std::string stats() override;
+  std::unique_ptr<Local> make_local(std::optional<int> port, std::optional<IpAddress> listen_address,
+                                    std::unique_ptr<Silo> storage) override;
+  int factor() const { return factor_; }
 
  protected:
-  void _store(const Block& b, StoreMode mode) override;
+  // Consensus::_store's loop (Consensus.cc:40-94): a Conflict goes to the
+  // resolver, whose block is stored instead, until it gives up.
+  void _store(std::unique_ptr<Block> block, StoreMode mode,
+              std::unique_ptr<ConflictResolver> resolver) override;
   using Consensus::_fetch;
-  std::unique_ptr<Block> _fetch(const Address& a) override;
+  // local_version: a mutable block no newer than it is not returned (null),
+  // as Paxos::_fetch with a local version does.
+  std::unique_ptr<Block> _fetch(Address address, std::optional<int> local_version) override;
   // Consensus::remove_many (Consensus.cc:178-240) over the `factor` replicas:
   // unreachable replicas are skipped, MissingBlock when none removed it.
   // (Mutable blocks' own remove validation is outside this path.)
-  void _remove(const Address& a, const RemoveSignature& rs) override;
+  void _remove(Address address, RemoveSignature rs) override;
 
  private:
   Overlay& overlay_;
   int factor_;
 };
+// The peer ReplicationConsensus::make_local makes, over `storage` (for a
+// network built before its consensus, as tests and benches do).
+std::unique_ptr<Local> make_replica_local(std::unique_ptr<Silo> storage);
+// The replica validation of ReplicationConsensus's peers (LocalPeer::store's
+// block->validate, Paxos.cc:1571-1575): a replica value of key k must decode,
+// and an immutable one must hash to k.  Throws ValidationFailed.
+void validate_replica(const Key& k, const uint8_t* v, size_t n);
 
 // ----------------------------------------------------------- configuration
 // consensus::Configuration (Consensus.hh:148-174): polymorphic, serialized

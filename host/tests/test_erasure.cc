@@ -72,6 +72,19 @@ bool wait_for(F pred, int ms = 20000) {
 
 Buffer bytes(const char* s) { return Buffer(s, s + std::strlen(s)); }
 
+// The reference's calls (Consensus.hh:38-49) for a test's block in hand:
+// store a copy, no conflict resolver; fetch many addresses, no versions;
+// remove with a signature or none.
+void store(Consensus& c, const Block& b, StoreMode mode = STORE_INSERT) {
+  c.store(std::make_unique<Block>(b), mode, nullptr);
+}
+void fetch_many(Consensus& c, const std::vector<Address>& as, const ReceiveBlock& res) {
+  std::vector<Consensus::AddressVersion> req;
+  for (auto& a : as) req.emplace_back(a, std::nullopt);
+  c.fetch(req, res);
+}
+void remove(Consensus& c, const Address& a, const RemoveSignature& rs = {}) { c.remove(a, rs); }
+
 Buffer random_bytes(size_t n, uint64_t seed) {
   std::mt19937_64 r(seed);
   Buffer b(n);
@@ -429,12 +442,12 @@ TEST(pinned_arena_drops_outsized_buffers, false) {
 TEST(CHB, true) {
   Net net(16, 10, 4);
   Block b = make_chb(bytes("\\_o<"));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.holders(b.address, 14) == 14);
   CHECK(net.ec->fetch(b.address)->data == b.data);
   auto f = net.ec->fetch(b.address);
   CHECK(f->data == b.data);
-  net.ec->remove(b.address);
+  remove(*net.ec, b.address);
   CHECK(net.shards(b.address, 14) == 0);
   CHECK_THROW(net.ec->fetch(b.address), MissingBlock);
 }
@@ -452,28 +465,28 @@ TEST(remove_owned_chb_semantics, true) {
   dir.set(owner, OwnerAcl{owner_k.public_key, {}, false, {}});
   net.ec->set_owner_directory(&dir);
   Block b = make_chb(random_bytes(70000, 77), bytes("salt"), owner);
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 14);
-  CHECK_THROW(net.ec->remove(b.address), ValidationFailed);
-  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove(b.address, other_k)), ValidationFailed);
+  CHECK_THROW(remove(*net.ec, b.address), ValidationFailed);
+  CHECK_THROW(remove(*net.ec, b.address, chb_sign_remove(b.address, other_k)), ValidationFailed);
   RemoveSignature forged = chb_sign_remove(b.address, owner_k);
   forged.signature_key = other_k.public_key;
-  CHECK_THROW(net.ec->remove(b.address, forged), ValidationFailed);
+  CHECK_THROW(remove(*net.ec, b.address, forged), ValidationFailed);
   CHECK(net.shards(b.address, 14) == 14);
   CHECK(net.ec->fetch(b.address)->data == b.data);
-  net.ec->remove(b.address, chb_sign_remove(b.address, owner_k));
+  remove(*net.ec, b.address, chb_sign_remove(b.address, owner_k));
   CHECK(net.shards(b.address, 14) == 0);
   CHECK_THROW(net.ec->fetch(b.address), MissingBlock);
-  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove(b.address, owner_k)), MissingBlock);
-  CHECK_THROW(net.ec->remove(Address::random(flags::immutable_block)), MissingBlock);
+  CHECK_THROW(remove(*net.ec, b.address, chb_sign_remove(b.address, owner_k)), MissingBlock);
+  CHECK_THROW(remove(*net.ec, Address::random(flags::immutable_block)), MissingBlock);
   // unowned blocks need no signature; a fresh client (no placement of the
   // block: a restart, index from the silos) removes them from the holders
   // lookup() names
   Block u = make_chb(random_bytes(5000, 78));
-  net.ec->store(u);
+  store(*net.ec, u);
   net.o.rescan = false;
   net.restart();
-  net.ec->remove(u.address);
+  remove(*net.ec, u.address);
   CHECK(net.shards(u.address, 14) == 0);
 }
 
@@ -484,8 +497,8 @@ TEST(remove_owned_chb_semantics, true) {
 TEST(remove_with_holder_down, true) {
   Net net(16, 10, 4);
   Block a = make_chb(random_bytes(40000, 90)), c = make_chb(random_bytes(40000, 91));
-  net.ec->store(a);
-  net.ec->store(c);
+  store(*net.ec, a);
+  store(*net.ec, c);
   std::shared_ptr<Node> down, back;
   for (auto& n : net.nodes)
     for (int i = 0; i < 14; ++i)
@@ -496,7 +509,7 @@ TEST(remove_with_holder_down, true) {
   CHECK(down && back);
   net.overlay.set_up(down->id, false);
   net.overlay.set_up(back->id, false);
-  net.ec->remove(a.address);
+  remove(*net.ec, a.address);
   CHECK(net.ec->pending_removes() == 2);
   // while holders are down a fetch cannot tell "removed" from "out of
   // reach" (as the single fetch with owners down: TooFewPeers)
@@ -568,7 +581,7 @@ static void chaos_run(uint64_t run_seed) {
       const int nb = op == 0 ? 1 + (int)(rng() % 40) : 1;
       for (int i = 0; i < nb; ++i) bs.push_back(make_chb(random_bytes(random_size(), ++seed)));
       if (op == 0) net.ec->store_many(bs);
-      else net.ec->store(bs[0]);
+      else store(*net.ec, bs[0]);
       for (auto& b : bs) live.emplace_back(b.address, b.data);
     } else if (op == 2) {  // a node goes down
       if (down_count() < m)
@@ -585,7 +598,7 @@ static void chaos_run(uint64_t run_seed) {
         }
     } else if (op == 5 && !live.empty()) {  // a removal
       const size_t x = rng() % live.size();
-      net.ec->remove(live[x].first);
+      remove(*net.ec, live[x].first);
       removed.push_back(live[x].first);
       live.erase(live.begin() + (long)x);
     } else if (op == 6 && !live.empty()) {  // one block alone
@@ -596,7 +609,7 @@ static void chaos_run(uint64_t run_seed) {
     std::vector<Address> req;
     for (auto& [a, d] : live) req.push_back(a);
     size_t ok = 0;
-    net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
+    fetch_many(*net.ec, req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
       for (auto& [x, d] : live)
         if (x == a && b && b->data == d) ++ok;
     });
@@ -689,7 +702,7 @@ TEST(multi_fetch_stages_in_chunks, true) {
   for (auto& b : blocks) req.push_back(b.address);
   const uint64_t seg0 = net.ec->codec().segments_calls(), leases0 = net.ec->arena_leases();
   int ok = 0;
-  net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
+  fetch_many(*net.ec, req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr) {
     for (auto& x : blocks)
       if (b && x.address == a && b->data == x.data) ++ok;
   });
@@ -709,17 +722,17 @@ TEST(missing_block, true) {
 // tests/doughnut.cc:840-846 (CHB_no_peer): no storage peer -> error.
 TEST(CHB_no_peer, true) {
   Net net(4, 10, 4);  // fewer reachable owners than k
-  CHECK_THROW(net.ec->store(make_chb(bytes("no peer"))), TooFewPeers);
+  CHECK_THROW(store(*net.ec, make_chb(bytes("no peer"))), TooFewPeers);
 }
 
 // Mutable blocks keep the backend (Paxos in memo) -- OKB, doughnut.cc:337-359.
 TEST(mutable_blocks_use_backend, true) {
   Net net(16, 10, 4);
   Block b = make_mutable(Address::random(flags::mutable_block), bytes("foo"));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.ec->fetch(b.address)->data == bytes("foo"));
   Block u = make_mutable(b.address, bytes("foobar"), 2);
-  net.ec->store(u, STORE_UPDATE);
+  store(*net.ec, u, STORE_UPDATE);
   CHECK(net.ec->fetch(b.address)->data == bytes("foobar"));
 }
 
@@ -749,7 +762,7 @@ TEST(resign_forwards_to_backend, true) {
   o.m = 4;
   ErasureConsensus ec(std::move(backend), overlay, o);
   Block b = make_chb(random_bytes(100000, 77));
-  ec.store(b);
+  store(ec, b);
   ec.resign();
   CHECK(bk->resigned == 1);
   int shards = 0;
@@ -766,7 +779,7 @@ TEST(availability, true) {
   for (size_t size : {size_t(1), size_t(1000), size_t(1) << 20, size_t(3000001)}) {
     Net net(14, 10, 4);
     Block b = make_chb(random_bytes(size, size));
-    net.ec->store(b);
+    store(*net.ec, b);
     auto owners = net.overlay.allocate(b.address, 14);
     // lose 4 owners, three of them holding data shards
     for (int i : {0, 3, 9, 12}) owners[i]->up = false;
@@ -789,7 +802,7 @@ TEST(multi_fetch_batches_decodes, true) {
     blocks.push_back(make_chb(random_bytes((i % 3 == 0 ? 4000 : i % 3 == 1 ? 60000 : 900000) + i, 100 + i)));
   net.ec->store_many(blocks);
   Block mut = make_mutable(Address::random(flags::mutable_block), bytes("meta"));
-  net.ec->store(mut);
+  store(*net.ec, mut);
   // two nodes down: many blocks lose data shards
   int down = 0;
   for (auto& n : net.nodes)
@@ -807,7 +820,7 @@ TEST(multi_fetch_batches_decodes, true) {
   const uint64_t leases0 = net.ec->arena_leases();
   std::vector<Address> seen;
   int ok = 0, missing_seen = 0;
-  net.ec->fetch(req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr e) {
+  fetch_many(*net.ec, req, [&](const Address& a, std::unique_ptr<Block> b, std::exception_ptr e) {
     seen.push_back(a);
     if (a == missing) {
       CHECK(!b && e);
@@ -861,7 +874,7 @@ TEST(multi_fetch_batches_decodes, true) {
 TEST(corrupted_shards_are_erasures, true) {
   Net net(14, 10, 4);
   Block b = make_chb(random_bytes(777777, 3));
-  net.ec->store(b);
+  store(*net.ec, b);
   int flipped = 0;
   for (auto& n : net.nodes)
     for (int i : {1, 2, 11, 13}) {
@@ -914,8 +927,8 @@ int64_t total_fetches(const Net& net) {
 TEST(reframed_shard_recovered_by_subset_retry, true) {
   Net net(16, 10, 4);
   Block b = make_chb(random_bytes(300000, 61)), c = make_chb(random_bytes(90000, 62));
-  net.ec->store(b);
-  net.ec->store(c);
+  store(*net.ec, b);
+  store(*net.ec, c);
   // a data shard: the first attempt decodes nothing and fails the address
   CHECK(reframe_shard(net, b.address, 3, 0xa5));
   CHECK(net.ec->fetch(b.address)->data == b.data);
@@ -937,14 +950,14 @@ TEST(reframed_shard_recovered_by_subset_retry, true) {
   // with the data holder back, the multi-fetch reassembles from the data
   // shards, needing no parity
   int got = 0;
-  net.ec->fetch(std::vector<Address>{c.address, b.address},
+  fetch_many(*net.ec, std::vector<Address>{c.address, b.address},
                 [&](const Address& a, std::unique_ptr<Block> blk, std::exception_ptr e) {
                   if (!e && blk && blk->data == (a == c.address ? c.data : b.data)) ++got;
                 });
   CHECK(got == 2);
   // one wrong parity shard in a degraded multi-fetch: recovered on the pool
   Block d = make_chb(random_bytes(120000, 63));
-  net.ec->store(d);
+  store(*net.ec, d);
   std::shared_ptr<Node> dd;
   for (auto& n : net.nodes)
     if (n->has(shard_key(d.address, 5))) dd = n;
@@ -954,7 +967,7 @@ TEST(reframed_shard_recovered_by_subset_retry, true) {
   net.overlay.set_up(dd->id, false);
   for (int r = 0; r < 4; ++r) {
     got = 0;
-    net.ec->fetch(std::vector<Address>{d.address},
+    fetch_many(*net.ec, std::vector<Address>{d.address},
                   [&](const Address&, std::unique_ptr<Block> blk, std::exception_ptr e) {
                     if (!e && blk && blk->data == d.data) ++got;
                   });
@@ -964,7 +977,7 @@ TEST(reframed_shard_recovered_by_subset_retry, true) {
   net.overlay.set_up(dd->id, true);
   // m + 1 = 5 wrong shards: no k-subset reassembles to the address
   Block e5 = make_chb(random_bytes(50000, 64));
-  net.ec->store(e5);
+  store(*net.ec, e5);
   for (int i : {0, 2, 4, 11, 13}) CHECK(reframe_shard(net, e5.address, i, 0x77));
   CHECK_THROW(net.ec->fetch(e5.address), ValidationFailed);
 }
@@ -982,7 +995,7 @@ TEST(degraded_fetch_reads_k_shards, true) {
       net.o.balanced_transfers = balanced;
       net.restart();
       Block b = make_chb(random_bytes(200000, 70 + hedge));
-      net.ec->store(b);
+      store(*net.ec, b);
       std::shared_ptr<Node> d2;
       std::map<int, std::shared_ptr<Node>> parity_holder;
       for (auto& n : net.nodes)
@@ -1050,7 +1063,7 @@ TEST(remove_unknown_block_reaches_every_holder, true) {
   auto rank = net.overlay.rank(b.address);
   net.overlay.set_up(rank[0]->id, false);
   net.overlay.set_up(rank[1]->id, false);
-  net.ec->store(b);
+  store(*net.ec, b);
   net.overlay.set_up(rank[0]->id, true);
   net.overlay.set_up(rank[1]->id, true);
   CHECK(net.shards(b.address, 14) == 14);
@@ -1058,7 +1071,7 @@ TEST(remove_unknown_block_reaches_every_holder, true) {
   ErasureOptions o = net.o;
   o.rescan = false;
   ErasureConsensus other(std::make_unique<ReplicationConsensus>(net.overlay, 3), net.overlay, o);
-  other.remove(b.address);
+  remove(other, b.address);
   CHECK(net.shards(b.address, 14) == 0);
 }
 
@@ -1070,16 +1083,16 @@ TEST(owed_removal_spares_restored_shard, true) {
   net.o.auto_expand = false;
   net.restart();
   Block b = make_chb(random_bytes(45000, 81));
-  net.ec->store(b);
+  store(*net.ec, b);
   std::shared_ptr<Node> h;
   for (auto& n : net.nodes)
     if (n->has(shard_key(b.address, 4))) h = n;
   CHECK(h != nullptr);
   net.overlay.set_up(h->id, false);
-  net.ec->remove(b.address);
+  remove(*net.ec, b.address);
   CHECK(net.ec->pending_removes() == 1);
   h->up = true;  // back, its return not yet signalled
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(h->has(shard_key(b.address, 4)) && net.shards(b.address, 14) == 14);
   h->up = false;
   net.overlay.set_up(h->id, true);  // the return: owed removals settle
@@ -1103,11 +1116,11 @@ TEST(remove_owned_chb_by_group_member, true) {
   dir.set(owner, OwnerAcl{owner_k.public_key, {}, false, {{G, true}, {R, false}}});
   net.ec->set_owner_directory(&dir);
   Block b = make_chb(random_bytes(33000, 82), bytes("salt"), owner);
-  net.ec->store(b);
-  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove_group(b.address, R, g2, 1)), ValidationFailed);
-  CHECK_THROW(net.ec->remove(b.address, chb_sign_remove_group(b.address, G, g1, 2)), ValidationFailed);
+  store(*net.ec, b);
+  CHECK_THROW(remove(*net.ec, b.address, chb_sign_remove_group(b.address, R, g2, 1)), ValidationFailed);
+  CHECK_THROW(remove(*net.ec, b.address, chb_sign_remove_group(b.address, G, g1, 2)), ValidationFailed);
   CHECK(net.shards(b.address, 14) == 14);
-  net.ec->remove(b.address, chb_sign_remove_group(b.address, G, g1, 1));
+  remove(*net.ec, b.address, chb_sign_remove_group(b.address, G, g1, 1));
   CHECK(net.shards(b.address, 14) == 0);
 }
 
@@ -1159,7 +1172,7 @@ TEST(CHB_unavailable, true) {
   Block b = make_chb(bytes("CHB_unavailable"));
   auto owners = net.overlay.allocate(b.address, 14);
   owners[2]->fail_stores = true;
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 13);
   CHECK(net.ec->under_placed() == 1);
   CHECK(net.ec->stats().find("\"under_placed\": 1") != std::string::npos);
@@ -1192,7 +1205,7 @@ TEST(evict_chain_expand, true) {
   });
   net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
   Block b = make_chb(random_bytes(5000, 2008));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.holders(b.address, 14) == 14);
   std::mt19937 rng(2008);
   for (int round = 0; round < 16; ++round) {
@@ -1232,7 +1245,7 @@ TEST(returning_node_takes_missing_shards, true) {
   auto away = net.nodes[5];
   net.overlay.set_up(away->id, false);
   Block b = make_chb(random_bytes(40000, 969));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 13);
   CHECK(wait_for([&] { return under.load() > 0; }));
   net.overlay.set_up(away->id, true);
@@ -1254,7 +1267,7 @@ TEST(retry_with_down_holders_and_free_nodes, true) {
   CHECK(spare.size() == 2);
   owners[13]->fail_stores = true;
   for (auto& n : spare) n->fail_stores = true;
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 13);
   // three holders go away silently; the free nodes start accepting
   for (int i = 0; i < 3; ++i) owners[i]->up = false;
@@ -1277,7 +1290,7 @@ TEST(evict_faulty, true) {
   std::atomic<int> rebalanced{0};
   net.ec->on_rebalanced([&](const Address&) { ++rebalanced; });
   Block b = make_chb(random_bytes(200000, 1651));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.holders(b.address, 14) == 14);
   auto d = net.add();  // fourth DHT: a discovery, nothing under-placed
   std::shared_ptr<Node> faulty;
@@ -1309,7 +1322,7 @@ TEST(expand_new_block, true) {
   auto owners = net.overlay.allocate(b.address, 14);
   owners[6]->fail_stores = true;
   owners[11]->fail_stores = true;
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 12);
   owners[6]->fail_stores = false;
   owners[11]->fail_stores = false;
@@ -1328,7 +1341,7 @@ TEST(concurrent_stores_batch_on_gpu, true) {
   std::vector<std::thread> ts;
   for (int t = 0; t < 16; ++t)
     ts.emplace_back([&, t] {
-      for (int i = t; i < 64; i += 16) net.ec->store(blocks[i]);
+      for (int i = t; i < 64; i += 16) store(*net.ec, blocks[i]);
     });
   for (auto& t : ts) t.join();
   const auto calls = net.ec->codec().encode_calls();
@@ -1403,7 +1416,7 @@ TEST(owned_chb_round_trip_degraded, true) {
   Net net(16, 10, 4);
   const Address owner = Address::random(flags::mutable_block);
   Block b = make_chb(random_bytes(300001, 41), bytes("salt!"), owner);
-  net.ec->store(b);
+  store(*net.ec, b);
   auto owners = net.overlay.allocate(b.address, 14);
   for (int i : {0, 2, 5, 13}) owners[i]->up = false;
   auto f = net.ec->fetch(b.address);
@@ -1433,7 +1446,7 @@ TEST(owned_chb_round_trip_degraded, true) {
 TEST(repair_rejects_foreign_shard, true) {
   Net net(20, 4, 2);
   Block b = make_chb(random_bytes(40000, 5));
-  net.ec->store(b);
+  store(*net.ec, b);
   auto owners = net.overlay.allocate(b.address, 6);
   // shard 1 replaced by a k = 2 shard of a 3x larger block, same address
   ShardHeader h;
@@ -1478,7 +1491,7 @@ TEST(expand_newcomer, true) {
     rebalanced.push_back(a);
   });
   Block b = make_chb(random_bytes(100000, 77));
-  net.ec->store(b);
+  store(*net.ec, b);
   CHECK(net.shards(b.address, 14) == 12);
   net.add();
   net.add();  // discovery -> rebalancing
@@ -1539,8 +1552,8 @@ TEST(evict_removed_blocks, true) {
   Net net(16, 10, 4, 200, /*eviction_delay_ms=*/150);
   std::vector<Block> bs;
   for (int i = 0; i < 3; ++i) bs.push_back(make_chb(random_bytes(50000, 900 + i)));
-  for (auto& b : bs) net.ec->store(b);
-  net.ec->remove(bs[1].address);
+  for (auto& b : bs) store(*net.ec, b);
+  remove(*net.ec, bs[1].address);
   CHECK(net.shards(bs[1].address, 14) == 0);
   std::shared_ptr<Node> a, c;
   for (auto& n : net.nodes) {
@@ -1655,7 +1668,7 @@ TEST(redundancy_json, true) {
   auto c = make_consensus(ov, "{\"type\": \"erasure\", \"data-shards\": 4, \"parity-shards\": 2}");
   CHECK(from_json(c->redundancy())["k"] == "4");
   Block b = make_chb(random_bytes(4096, 9));
-  c->store(b);
+  store(*c, b);
   CHECK(c->fetch(b.address)->data == b.data);
 }
 

@@ -481,15 +481,30 @@ def test_plugin_lines_parse_and_flag_failures(tmp_path):
     kept whole, a non-zero exit or a missing rate marks the row not ok with
     the child's stderr, and a missing binary is a note, not a crash."""
     import bench
-    line = json.dumps({"workload": "x", "erasure": {k: 1.0 for k in bench.PLUGIN_KEYS} | {
-        "fetch_after_repair_ok": True, "unrecoverable": 0}, "replication": {"fetch_GiBs": 2.0}})
+    line = json.dumps({"workload": "x", "reps": 5,
+                       "erasure": {k: [1.0, 3.0, 2.0, 5.0, 4.0] for k in bench.PLUGIN_KEYS} | {
+                           "fetch_after_repair_ok": True, "unrecoverable": 0},
+                       "replication": {"store_GiBs": [2.0, 2.0, 2.0, 2.0, 2.0],
+                                       "fetch_GiBs": [1.0, 1.0, 4.0, 1.0, 1.0]}})
     fake = tmp_path / "bench_plugin"
     fake.write_text("#!/bin/sh\n[ \"$1\" = 3 ] && { echo oops >&2; echo '%s'; exit 1; }\n"
-                    "[ \"$1\" = 5 ] && { echo '{\"erasure\": {}}'; exit 0; }\necho '%s'\n" % (line, line))
+                    "[ \"$1\" = 5 ] && { echo '{\"erasure\": {}}'; exit 0; }\n"
+                    "[ \"$3\" = 5 ] || exit 9\necho '%s'\n" % (line, line))
     fake.chmod(0o755)
     out = bench.plugin_lines(str(fake), [(2, 4096), (3, 4096), (5, 64)], timeout=30)
-    assert out["2x4096"]["ok"] and out["2x4096"]["erasure"]["fetch_after_repair_ok"]
-    assert out["2x4096"]["replication"]["fetch_GiBs"] == 2.0
+    row = out["2x4096"]
+    assert row["ok"] and row["erasure"]["fetch_after_repair_ok"] and row["reps"] == 5
+    # {median, min, max, n} per rate, from the five repetitions
+    st = row["erasure"]["store_GiBs"]
+    assert (st["median"], st["min"], st["max"], st["n"]) == (3.0, 1.0, 5.0, 5)
+    assert st["samples"] == [1.0, 3.0, 2.0, 5.0, 4.0]
+    assert row["replication"]["fetch_GiBs"]["median"] == 1.0
+    assert row["replication"]["fetch_GiBs"]["max"] == 4.0
+    # ratios per repetition (erasure / replication of the same repetition)
+    assert row["ratio"]["store"]["samples"] == [0.5, 1.5, 1.0, 2.5, 2.0]
+    assert row["ratio"]["store"]["median"] == 1.5
+    assert row["ratio"]["fetch"]["samples"] == [1.0, 3.0, 0.5, 5.0, 4.0]
+    assert row["ratio"]["fetch"]["median"] == 3.0 and row["ratio"]["fetch"]["min"] == 0.5
     assert not out["3x4096"]["ok"] and "oops" in out["3x4096"]["note"]
     assert not out["5x64"]["ok"]
     gone = bench.plugin_lines(str(tmp_path / "missing"), [(1, 1)], timeout=30)
