@@ -1147,6 +1147,57 @@ def skipped_at_n(args, world):
     return out
 
 
+# Rates behind post_timed_seconds, measured on the GPU boxes: the oracle
+# port's single-core encode (BENCH_r05.json cpu_baseline.single_core: 27.1
+# GiB/s; its rebuild is faster), the pinned device-to-host rate one link
+# gives a staged 256 MiB chunk while every link of the node is busy (DESIGN
+# §6: 49.4 GiB/s both directions on one link; half of it taken here), the
+# seconds of one rocprofv3 counter pass (a child bench.py: torch import,
+# fill, a few launches; tens of seconds on a fresh box), the PCIe
+# end-to-end leg and the in-library stream probe.
+POST_RATES = {"oracle_core_GiBs": 27.0, "dtoh_GiBs": 20.0, "pmc_pass_s": 60.0, "e2e_s": 10.0,
+              "probe_s": 3.0, "c1_s": 5.0, "startup_s": 120.0}
+
+
+def post_timed_seconds(args, world, threads_per_rank, S, rates=POST_RATES):
+    """Estimated seconds a rank spends outside the timed steps at `world`
+    ranks with `threads_per_rank` CPU threads each (main: the job's CPU share
+    split over the ranks): start-up (torch import, inputs), the stream probe,
+    the whole-batch oracle checks of its own C2 / C3 batches (staged over its
+    own link, recomputed on its threads), the PCIe end-to-end leg, and on
+    rank 0 the CPU baseline, C1 and the counter passes.  The N = 1-only legs
+    (4 KiB lines, C5, plugin, SHA-256) are not run at N > 1.  Returns
+    {"rank": s, "rank0": s, "legs": {...}} to hold against --rank-timeout."""
+    k, m, n, e = args.k, args.m, args.blocks, args.erasures
+    gib = float(1 << 30)
+    legs = {"startup": rates["startup_s"], "probe": rates["probe_s"]}
+    if not args.no_verify:
+        core = rates["oracle_core_GiBs"] * max(1, threads_per_rank)
+        c2 = n * (k + m) * S / gib / rates["dtoh_GiBs"] + n * k * S / gib / core
+        c3 = n * (k + e) * S / gib / rates["dtoh_GiBs"] + n * k * S / gib / core if e > 0 else 0.0
+        legs["oracle_checks"] = c2 + c3
+    if not args.no_e2e:
+        legs["end_to_end"] = rates["e2e_s"]
+    rank = sum(legs.values())
+    r0 = dict(legs)
+    if not args.no_cpu:
+        r0["cpu_baseline"] = args.cpu_seconds * 1.5  # the timed sample, its setup and the scalar oracle
+        r0["c1"] = rates["c1_s"]
+    if not args.no_pmc:
+        r0["counter_passes"] = 2 * rates["pmc_pass_s"]
+    if world == 1:
+        if not args.no_small:
+            r0["rebuild_small"] = 60.0
+        if not args.no_c5:
+            r0["c5_mixed"] = 30.0
+        if not args.no_plugin:
+            r0["plugin"] = 120.0
+        if not args.no_sha:
+            r0["sha256"] = 20.0
+    return {"rank": round(rank, 2), "rank0": round(sum(r0.values()), 2),
+            "legs": {k_: round(v, 2) for k_, v in r0.items()}}
+
+
 def assemble(args, world, rows, wall_max, S):
     """The contract line from the ranks' rows (pure: tested on CPU)."""
     from memo_amd.partition import node_report

@@ -1409,14 +1409,29 @@ std::vector<std::vector<int>> retry_subsets(int n, int k, int limit) {
 // disagrees with the verified block is rewritten on its holder.
 std::unique_ptr<Block> ErasureConsensus::recover(const Address& a, bool parallel) {
   const int k = o_.k, m = o_.m, total = k + m;
+  // k + 1 shards first (one spare out-votes one wrong shard, and a holder
+  // that is down does not send the gather over the whole membership), all
+  // of them when that finds no good subset
+  if (k + 1 < total)
+    if (auto b = recover_from(a, k + 1, parallel)) return b;
+  if (auto b = recover_from(a, total, parallel)) return b;
+  throw AddressMismatch("erasure: reassembled block does not match its address (no k-subset of the "
+                        "reachable shards matches)");
+}
+
+std::unique_ptr<Block> ErasureConsensus::recover_from(const Address& a, int want, bool parallel) {
+  const int k = o_.k, m = o_.m, total = k + m;
   const std::string what = "erasure: reassembled block does not match its address";
   bool any_down = false;
   ShardHeader h;
   std::vector<Node*> from(total, nullptr);
-  auto have = gather_shards(a, total, any_down, &h, parallel, &from);
+  auto have = gather_shards(a, want, any_down, &h, parallel, &from);
   std::sort(have.begin(), have.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
   const int n = (int)have.size();
-  if (n <= k) throw AddressMismatch(what + " (no spare shard to try)");
+  if (n <= k) {
+    if (want < total) return nullptr;  // the wider gather may find more
+    throw AddressMismatch(what + " (no spare shard to try)");
+  }
   const size_t S = h.shard_size;
   std::vector<uint8_t> sidx(k), lost;
   Buffer surv((size_t)k * S), out((size_t)m * S), block;
@@ -1469,6 +1484,7 @@ std::unique_ptr<Block> ErasureConsensus::recover(const Address& a, bool parallel
     b->owner = h.owner;
     return b;
   }
+  if (want < total) return nullptr;
   throw AddressMismatch(what + " (no k-subset of the " + std::to_string(n) +
                         " reachable shards matches)");
 }
@@ -1750,7 +1766,7 @@ void ErasureConsensus::_remove(Address a, RemoveSignature rs) {
         // the debt when it is evicted), so the block does not come back with
         // it.  For a block of unknown placement, every index it might hold.
         std::lock_guard<std::mutex> g(emu);
-        for (int j = i; j < i1; ++j) deferred.push_back({nd->id, OwedRemove{a, j}});
+        deferred.push_back({nd->id, OwedRemove{a, targets[t].index < 0 ? -1 : i, rs}});
         break;
       } catch (silo::MissingKey&) {
       }
@@ -1777,7 +1793,11 @@ size_t ErasureConsensus::pending_removes() const {
 }
 
 // Shards a removal could not reach on `node` (down at the time): erased now
-// that it is back, or forgotten with its silo when it is evicted.
+// that it is back, or forgotten with its silo when it is evicted.  A shard
+// is kept when the block lives again: stored again with this node holding
+// it (this client's index), or with shards of it on other nodes (another
+// client stored it after the removal); and when the removal's signature no
+// longer validates against the owner its header records.
 void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
   std::vector<OwedRemove> owed;
   {
@@ -1789,22 +1809,41 @@ void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
   }
   if (evicted) return;
   auto nd = overlay_.node(node);
+  if (!nd) return;
+  const int total = o_.k + o_.m;
   std::vector<OwedRemove> still;
   for (auto& r : owed) {
     // the block was stored again with this node holding that shard (a CHB
     // key is its content's): the shard is live, the debt is void
+    bool restored = false;
     {
       std::shared_lock<std::shared_mutex> g(index_mu_);
       auto it = index_.find(r.block);
-      if (it != index_.end() && r.index < (int)it->second.holder.size() &&
-          it->second.holder[r.index] == node)
-        continue;
+      if (it != index_.end())
+        for (int i = 0; i < (int)it->second.holder.size(); ++i)
+          restored = restored || ((r.index < 0 || r.index == i) && it->second.holder[i] == node);
     }
+    if (restored) continue;
     try {
-      if (nd) nd->remove(shard_key(r.block, r.index));
+      if (held_elsewhere(r.block, node)) continue;  // stored again by another client
+      const ShardKeys keys(r.block);
+      for (int i = r.index < 0 ? 0 : r.index; i < (r.index < 0 ? total : r.index + 1); ++i) {
+        Buffer head;
+        if (!nd->try_fetch_prefix(keys(i), ShardHeader::kSize, head)) continue;
+        Address shard_owner;
+        try {
+          shard_owner = decode_shard_header(head.data(), head.size()).owner;
+        } catch (ValidationFailed&) {
+          // no shard of any block under this key: removed
+        }
+        if (!chb_validate_remove(r.block, shard_owner, r.rs, owners_).empty()) continue;
+        try {
+          nd->remove(keys(i));
+        } catch (silo::MissingKey&) {
+        }
+      }
     } catch (Unavailable&) {
       still.push_back(r);  // down again
-    } catch (silo::MissingKey&) {
     }
   }
   if (!still.empty()) {
@@ -1812,6 +1851,17 @@ void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
     auto& v = pending_rm_[node];
     v.insert(v.end(), still.begin(), still.end());
   }
+}
+
+bool ErasureConsensus::held_elsewhere(const Address& a, const Address& except) const {
+  const int total = o_.k + o_.m;
+  const ShardKeys keys(a);
+  for (auto& nd : overlay_.lookup(a, (int)overlay_.size())) {
+    if (nd->id == except || !nd->up) continue;
+    for (int i = 0; i < total; ++i)
+      if (nd->has(keys(i))) return true;
+  }
+  return false;
 }
 
 // ------------------------------------------------------------- repair

@@ -473,6 +473,9 @@ class ErasureConsensus : public StackedConsensus {
   // its reachable shards; the disagreeing shards rewritten (AddressMismatch
   // when no subset within verify_subsets matches).
   std::unique_ptr<Block> recover(const Address& a, bool parallel);
+  // recover() from the first `want` shards gathered: null when none of its
+  // subsets matches and a wider gather is left to try
+  std::unique_ptr<Block> recover_from(const Address& a, int want, bool parallel);
   // index_ updates under index_mu_ (held exclusively by the caller); they
   // return the block's previous holders for the node index, which the
   // caller updates after releasing the lock
@@ -525,12 +528,18 @@ class ErasureConsensus : public StackedConsensus {
   std::atomic<uint64_t> subset_recoveries_{0}, corrupt_rewritten_{0};
   const OwnerDirectory* owners_ = nullptr;
   mutable std::mutex rm_mu_;
-  // Shard removals owed to a node that was down: the block and shard index
-  // (so a returning node keeps a shard the block was stored again with)
+  // Shard removals owed to a node that was down: the block, the shard index
+  // (-1: every index, for a block of unknown placement -- one record per
+  // (node, block)) and the removal's signature, validated again against the
+  // shard's header when the node returns
   struct OwedRemove {
     Address block;
     int index;
+    RemoveSignature rs;
   };
+  // Whether some node other than `except` holds a shard of `a` (a block
+  // stored again after its removal).
+  bool held_elsewhere(const Address& a, const Address& except) const;
   std::map<Address, std::vector<OwedRemove>> pending_rm_;  // node -> removals still owed
   // in-flight fetches from this client per node (the reference's
   // Paxos::_transfers), hashed into per-thread-slot counters: every shard

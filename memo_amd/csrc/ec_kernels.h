@@ -41,7 +41,8 @@ constexpr int DEC_IDX_REGS = 2;
 // MAC_IMAGES: a rebuild over per-block table images -- the encode's code
 // under a kernel name of its own (gf_mac_images_kernel), so traces tell a
 // rebuild MAC from an encode.
-enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2, MAC_PROBE = 3, MAC_IMAGES = 4 };
+enum MacMode : int { MAC_ENCODE = 0, MAC_ROWS = 1, MAC_FUSED = 2, MAC_PROBE = 3, MAC_IMAGES = 4,
+                     MAC_PERM = 5 /* MEMO_EC_PERM_PROBE builds only (tools/perm_probe.py) */ };
 
 // LDS bytes of the fused rebuild's decode workspace for a tile of ns blocks:
 // GF log/antilog (1 KiB), LW0 (128 B), per block 3 survivor-mask words + a

@@ -924,6 +924,41 @@ __device__ __forceinline__ void mac_tile(const MacSeg& sg, uint64_t tile, uint32
         mac_chunk<KC, R>(acc, d, tab, kpad, j0);
       }
     }
+#ifdef MEMO_EC_PERM_PROBE
+  } else if constexpr (MODE == MAC_PERM) {
+    // Probe only (tools/perm_probe.py): each block's
+    // images come from a per-code table of every erasure pattern's product
+    // images (q: 16 B, lo: 4 B per slot), indexed by the block's pattern
+    // rank (sg.coef: one u16 per block), instead of being built from decode
+    // rows.  Ranks first, the shard loads, then the image loads.
+    const uint32_t per = R * KC, total = u.nsets * per, t = threadIdx.x;
+    const uint16_t* prank = reinterpret_cast<const uint16_t*>(sg.coef);
+    uint32_t pr[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const uint32_t ci = t + 256u * q, set = ci < total ? ci / per : 0u;
+      pr[q] = prank[u.b_first + set];
+    }
+    uint4 d[KC];
+#pragma unroll
+    for (int g = 0; g < KC; ++g) d[g] = ld16<NT>(u.in(sg, g));
+    const uint4* qt = reinterpret_cast<const uint4*>(sg.tab);
+    const uint32_t* lt = reinterpret_cast<const uint32_t*>(sg.sidx);
+    uint4 qv[6];
+    uint32_t lv[6];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const uint32_t ci = t + 256u * q;
+      const uint64_t off = (uint64_t)pr[q] * per + (ci < total ? ci % per : 0u);
+      qv[q] = qt[off];
+      lv[q] = lt[off];
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      if (t + 256u * q < total) put_image(s_tab, sg, per, t + 256u * q, qv[q], lv[q]);
+    __syncthreads();
+    mac_chunk<KC, R>(acc, d, tab, kpad, 0);
+#endif
   } else if (kin == KC) {
     // Hot path.  The table image loads go out first (vmcnt retires in issue
     // order, so the LDS copy then waits only for them), the KC shard loads
@@ -991,6 +1026,17 @@ __global__ void __launch_bounds__(256) gf_mac_images_kernel(const MacLaunch L) {
   if (!seg_tile(L, sid, tile)) return;
   mac_tile<KC, R, NT, MAC_ENCODE>(L.seg[sid], tile, s_tab);
 }
+
+#ifdef MEMO_EC_PERM_PROBE
+template <int KC, int R, bool NT>
+__global__ void __launch_bounds__(256) gf_mac_perm_kernel(const MacLaunch L) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t s_tab[];
+  uint32_t sid;
+  uint64_t tile;
+  if (!seg_tile(L, sid, tile)) return;
+  mac_tile<KC, R, NT, MAC_PERM>(L.seg[sid], tile, s_tab);
+}
+#endif
 
 // Rebuild in one launch: decode rows derived per tile, then the MAC.
 template <int KC, int R, bool NT>
@@ -1861,6 +1907,10 @@ static hipError_t launch_mac_t(int mode, const MacLaunch& L, uint32_t grid, size
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, true>), dim3(grid), dim3(256), lds, st, L);
   else if (mode == MAC_IMAGES)
     hipLaunchKernelGGL((gf_mac_images_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
+#ifdef MEMO_EC_PERM_PROBE
+  else if (mode == MAC_PERM)
+    hipLaunchKernelGGL((gf_mac_perm_kernel<KC, R, MAC_NT>), dim3(grid), dim3(256), lds, st, L);
+#endif
   else
     hipLaunchKernelGGL((gf_mac_kernel<KC, R, MAC_NT, false>), dim3(grid), dim3(256), lds, st, L);
   return hipGetLastError();

@@ -1151,19 +1151,20 @@ int launch_rebuild_pieces(memo_ec_ctx* c, const std::vector<RPiece>& ps, uint8_t
   size_t ndec = 0;
   for (const auto& k : cls) ndec += !k.dec.empty();
   if (ndec > 1 && c->opt.decode_overlap) {
+    if (int rc = side_events(c, (int)ndec + 1)) return rc;
+    // the side stream starts after the call's stream's earlier work, and
+    // beside the first class's decode (recorded before it: the side decodes
+    // do not depend on it)
+    HIPCHK(hipEventRecord(c->side_ev[0], st));
+    HIPCHK(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
     bool first = true;
     int ne = 0;
     for (size_t x = 0; x < cls.size(); ++x) {
       if (cls[x].dec.empty()) continue;
-      if (first) {  // nothing runs before it to overlap with
+      if (first) {  // on the call's stream, before its own MAC
         HIPCHK(launch_decode_multi(cls[x].dec.data(), (int)cls[x].dec.size(), st));
         first = false;
         continue;
-      }
-      if (int rc = side_events(c, ne + 2)) return rc;
-      if (ne == 0) {  // the side stream starts after the call's stream's earlier work
-        HIPCHK(hipEventRecord(c->side_ev[0], st));
-        HIPCHK(hipStreamWaitEvent(c->side, c->side_ev[0], 0));
       }
       HIPCHK(launch_decode_multi(cls[x].dec.data(), (int)cls[x].dec.size(), c->side));
       HIPCHK(hipEventRecord(c->side_ev[ne + 1], c->side));
@@ -1449,6 +1450,33 @@ int memo_ec_stream_probe(memo_ec_ctx* c, int kin, int r, size_t S, size_t n, con
   }
   return MEMO_EC_OK;
 }
+
+#ifdef MEMO_EC_PERM_PROBE
+// Probe only (tools/perm_probe.py; not in include/memo_ec.h): the rows MAC
+// of n per-block-pattern blocks (e = m lost, survivors and lost shards in
+// ascending order) with each block's product images read from a per-code
+// table of every pattern's images (qtab: uint4, lotab: dword, R x k slots
+// per pattern) at the block's pattern rank (prank[b], u16), instead of
+// built from decode rows.  Device pointers; asynchronous on the ctx stream.
+extern "C" int memo_ec_probe_perm_mac(memo_ec_ctx* c, int k, int m, size_t S, size_t n,
+                                      const uint8_t* surv, uint8_t* out, const uint16_t* prank,
+                                      const uint32_t* qtab, const uint32_t* lotab) {
+  if (!c || !surv || !out || !prank || !qtab || !lotab) return MEMO_EC_EINVAL;
+  if (int rc = check_km(k, m)) return rc;
+  DeviceGuard g(c->device);
+  const int e = m, R = mac_rbound(e), KC = mac_kchunk(k, R);
+  if (KC != k || R != e) return MEMO_EC_EINVAL;  // the straight-line bodies only
+  Plan p = plan_segment((uint32_t)k, (uint32_t)e, S, n, surv, (uint64_t)k * S, S, out, (uint64_t)e * S, S,
+                        nullptr, 0, KC, R, reinterpret_cast<const uint8_t*>(prank), 1, (uint32_t)e);
+  if (!p.seg.flat || sets_per_tile(p.seg.chunks) * (uint64_t)R * k > 6 * 256) return MEMO_EC_ERANGE;
+  p.mode = MAC_PERM;
+  p.seg.coef_dense = 0;
+  p.seg.tab = qtab;
+  p.seg.sidx = reinterpret_cast<const uint8_t*>(lotab);
+  std::vector<Plan> plans{p};
+  return launch_plans(c, plans, c->stream);
+}
+#endif
 
 void* memo_ec_host_alloc(size_t bytes) {
   void* p = nullptr;

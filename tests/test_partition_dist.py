@@ -205,6 +205,46 @@ def test_bench_assemble_world_8_c4_line():
         bench.assemble(args, 8, dup, 0.021, S)
 
 
+def test_world_8_line_fits_the_rank_lease(monkeypatch):
+    """The 8-GPU line (C4) with the job's CPU share split 8 ways (16 CPUs:
+    2 threads per rank) still fits --rank-timeout: the whole-batch oracle
+    checks of every rank's own 4096 x 1 MiB C2 / C3 batches, the CPU
+    baseline and the counter passes on rank 0 -- estimated from the rates
+    measured on the GPU boxes (bench.POST_RATES) -- plus the timed steps;
+    and assemble() turns the eight rows into the line."""
+    import bench
+    monkeypatch.setattr(bench, "host_cores", lambda: 256)
+    monkeypatch.setattr(bench, "_cgroup_cpus", lambda: 16)
+    monkeypatch.delenv("OMP_NUM_THREADS", raising=False)
+    args = bench.parse(["--gpus", "8"])
+    world, S = 8, 104896
+    per_rank = max(1, bench.cpu_threads(world) // world)   # what main() gives each rank's checks
+    assert per_rank == 2
+    est = bench.post_timed_seconds(args, world, per_rank, S)
+    timed = (args.warmup + args.steps) * 2.0e-3 + args.settle_ms * 1e-3
+    assert est["rank0"] + timed < args.rank_timeout, est
+    assert est["rank"] <= est["rank0"]
+    assert set(est["legs"]) >= {"oracle_checks", "cpu_baseline", "counter_passes"}
+    assert not {"rebuild_small", "c5_mixed", "plugin", "sha256"} & set(est["legs"])
+    # one thread per rank (a 8-CPU share) still fits; the N = 1 line, with
+    # every leg, fits its own lease on the box's 16 threads
+    assert bench.post_timed_seconds(args, world, 1, S)["rank0"] + timed < args.rank_timeout
+    one = bench.parse(["--gpus", "1"])
+    assert bench.post_timed_seconds(one, 1, 16, S)["rank0"] + timed < one.rank_timeout
+    # a slower box (half the rates, twice the pass times) still fits at N = 8
+    slow = {k: (v / 2 if k.endswith("GiBs") else v * 2) for k, v in bench.POST_RATES.items()}
+    assert bench.post_timed_seconds(args, world, per_rank, S, slow)["rank0"] + timed < args.rank_timeout
+    rows = [{"rank": r, "device": r, "warmup_steps_run": 40,
+             "device_identity": {"pci_bus_id": "0000:%02x:00.0" % (0x05 + 0x10 * r), "uuid": "%032x" % (0xa0 + r)},
+             "payload_bytes": args.blocks * args.block_bytes * 2 * args.steps,
+             "device_seconds": 2.0e-3 * args.steps,
+             "encode": bench.kstats([0.98] * args.steps, 14 * S * args.blocks),
+             "rebuild": bench.kstats([1.0] * args.steps, 14 * S * args.blocks),
+             "rebuild_bit_exact": True, "rebuild_kernel": "gf_mac_images_kernel"} for r in range(world)]
+    res = bench.assemble(args, world, rows, 2.0e-3 * args.steps, S)
+    assert res["n_gpus"] == 8 and res["ranks"]["distinct_devices"] == 8
+
+
 def test_cpu_share_is_bounded(monkeypatch):
     """The CPU baseline's threads: at N = 1 the affinity set capped by the
     cgroup quota and OMP_NUM_THREADS; at N > 1 the job's node share (the
