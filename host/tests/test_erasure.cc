@@ -113,7 +113,9 @@ struct Net {
     uint8_t id[32] = {0};
     id[0] = (uint8_t)(nodes.size() + 1);
     id[1] = 0x4d;
-    nodes.push_back(overlay.add_node(Address(id, 0, false), std::make_unique<MemorySilo>()));
+    // the node's peer is the erasure consensus's (ErasureConsensus::make_local
+    // over a replication backend): shards checked by header, CRC and key
+    nodes.push_back(overlay.add_node(Address(id, 0, false), make_shard_local(std::make_unique<MemorySilo>())));
     return nodes.back();
   }
   // A fresh consensus over the same silos (a node restart): its index comes
@@ -277,6 +279,98 @@ TEST(config_registry, false) {
   CHECK_THROW(make_consensus(ov, "{\"type\": \"erasure\", \"threads\": 0}"), Error);
   auto r = make_consensus(ov, "{\"type\": \"replication\", \"replication-factor\": 2}");
   CHECK(from_json(r->redundancy())["type"] == "replication");
+}
+
+// The peers the consensuses make (Consensus::make_local, Consensus.hh:100-
+// 105): what LocalPeer::store validates (Paxos.cc:1568-1615), restated.
+TEST(peers_validate_what_they_store, false) {
+  // replication's peer: a CHB replica must hash to its key
+  Overlay ov;
+  ReplicationConsensus rc(ov, 2);
+  auto a = ov.add_node(Address::random(0), rc.make_local(7000, IpAddress{"127.0.0.1"}, std::make_unique<MemorySilo>()));
+  auto b = ov.add_node(Address::random(0), rc.make_local({}, {}, std::make_unique<MemorySilo>()));
+  CHECK(a->local->port() == 7000 && a->local->listen_address()->text == "127.0.0.1");
+  Block good = make_chb(bytes("payload"));
+  store(rc, good);
+  CHECK(rc.fetch(good.address)->data == good.data);
+  Block forged = make_chb(bytes("payload"));
+  forged.data = bytes("other bytes");  // the address no longer its content's
+  CHECK_THROW(store(rc, forged), ValidationFailed);
+  // a mutable block's version must grow: Conflict, resolved by the resolver
+  Block m1 = make_mutable(Address::random(flags::mutable_block), bytes("v1"), 1);
+  store(rc, m1);
+  Block m1b = make_mutable(m1.address, bytes("v1 again"), 1);
+  CHECK_THROW(store(rc, m1b, STORE_UPDATE), Conflict);
+  struct Bump : ConflictResolver {
+    int* calls;
+    explicit Bump(int* c) : calls(c) {}
+    std::unique_ptr<Block> operator()(Block& failed, Block& current) override {
+      ++*calls;
+      auto nb = std::make_unique<Block>(failed);
+      nb->version = current.version + 1;
+      return nb;
+    }
+    std::string description() const override { return "bump"; }
+  };
+  int calls = 0;  // the resolver is the store's (unique_ptr): count outside it
+  rc.store(std::make_unique<Block>(m1b), STORE_UPDATE, std::make_unique<Bump>(&calls));
+  CHECK(calls == 1);
+  auto got = rc.fetch(m1.address);
+  CHECK(got->data == bytes("v1 again") && got->version == 2);
+  CHECK(rc.fetch(m1.address, 2) == nullptr);  // not newer than the caller's version
+  CHECK(rc.fetch(m1.address, 1)->version == 2);
+  // the erasure peer: shards by header, CRC and key; other values to the
+  // replication peer's checks
+  auto local = make_shard_local(std::make_unique<MemorySilo>());
+  ShardHeader h;
+  h.k = 10;
+  h.m = 4;
+  h.index = 3;
+  h.block_size = 5000;
+  h.shard_size = memo_ec_shard_size(5000, 10);
+  h.address = good.address;
+  const Buffer pay = random_bytes(h.shard_size, 5);
+  Buffer w = encode_shard(h, pay.data());
+  local->validate(shard_key(h.address, 3), w.data(), w.size());  // accepted
+  CHECK_THROW(local->validate(shard_key(h.address, 4), w.data(), w.size()), ValidationFailed);
+  Buffer bad = w;
+  bad[ShardHeader::kSize + 17] ^= 1;
+  CHECK_THROW(local->validate(shard_key(h.address, 3), bad.data(), bad.size()), ValidationFailed);
+  // a shard may only replace a shard
+  local->storage().set(shard_key(h.address, 3), bytes("not a shard"));
+  CHECK_THROW(local->validate(shard_key(h.address, 3), w.data(), w.size()), ValidationFailed);
+  Buffer rep(40, 0);  // an empty CHB replica under the wrong key
+  CHECK_THROW(local->validate(good.address, rep.data(), rep.size()), ValidationFailed);
+  // through a node: the refused value never reaches the silo
+  Overlay ov2;
+  auto n = ov2.add_node(Address::random(0), make_shard_local(std::make_unique<MemorySilo>()));
+  CHECK_THROW(n->store(shard_key(h.address, 3), bad), ValidationFailed);
+  CHECK(!n->has(shard_key(h.address, 3)));
+  n->store(shard_key(h.address, 3), w);
+  CHECK(n->has(shard_key(h.address, 3)));
+}
+
+// The stack and the factory (Consensus.hh:100-142): find<C> walks the
+// stack, make_remote is the backend's, stat reports the placement.
+TEST(stacked_consensus_surface, true) {
+  Overlay ov;
+  ErasureOptions o;
+  o.k = 4;
+  o.m = 2;
+  o.device = 0;
+  auto ec = std::unique_ptr<Consensus>(new ErasureConsensus(std::make_unique<ReplicationConsensus>(ov, 3), ov, o));
+  CHECK(StackedConsensus::find<ErasureConsensus>(ec.get()) == ec.get());
+  auto* rep = StackedConsensus::find<ReplicationConsensus>(ec.get());
+  CHECK(rep != nullptr && rep->factor() == 3);
+  CHECK(StackedConsensus::find<ReplicationConsensus>(rep) == rep);
+  auto conn = std::make_shared<DockConnection>();
+  conn->peer = Address::random(0);
+  auto remote = ec->make_remote(conn);
+  CHECK(remote && remote->id() == conn->peer);
+  auto st = from_json(ec->stat(Address::random(flags::immutable_block))->json());
+  CHECK(st["placed"] == "0" && st["k"] == "4" && st["m"] == "2");
+  auto local = ec->make_local(9000, {}, std::make_unique<MemorySilo>());
+  CHECK(dynamic_cast<ShardLocal*>(local.get()) != nullptr && local->port() == 9000);
 }
 
 TEST(placement_is_deterministic_and_distinct, false) {
@@ -444,6 +538,8 @@ TEST(CHB, true) {
   Block b = make_chb(bytes("\\_o<"));
   store(*net.ec, b);
   CHECK(net.holders(b.address, 14) == 14);
+  auto st = from_json(net.ec->stat(b.address)->json());  // Consensus::stat
+  CHECK(st["placed"] == "1" && st["reachable"] == "14" && st["block_size"] == "4");
   CHECK(net.ec->fetch(b.address)->data == b.data);
   auto f = net.ec->fetch(b.address);
   CHECK(f->data == b.data);
