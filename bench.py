@@ -914,22 +914,27 @@ def spread(samples):
 
 def plugin_aggregate(d):
     """The child's per-repetition lists -> {median, min, max, n} per rate, and
-    the erasure / replication ratio of each repetition (the two ran
-    back to back in that repetition, so the ratio cancels box drift) for
-    store and fetch."""
+    the erasure / replication ratio of each repetition (the sides ran back
+    to back in that repetition, so the ratio cancels box drift) for store
+    and fetch: against replication through validating peers (`ratio`) and
+    through plain peers (`ratio_unvalidated`, the rounds 1-5 baseline)."""
     er, rp = dict(d.get("erasure", {})), dict(d.get("replication", {}))
-    for side in (er, rp):
+    ru = dict(d.get("replication_unvalidated", {}))
+    for side in (er, rp, ru):
         for key, val in list(side.items()):
             if key.endswith("_GiBs") and isinstance(val, list) and val:
                 side[key] = spread(val)
-    ratio = {}
-    for key in ("store_GiBs", "fetch_GiBs"):
-        a, b = er.get(key), rp.get(key)
-        if isinstance(a, dict) and isinstance(b, dict) and a["n"] == b["n"]:
-            per = [x / y for x, y in zip(a["samples"], b["samples"]) if y > 0]
-            if len(per) == a["n"]:
-                ratio[key.replace("_GiBs", "")] = spread(per)
-    return er, rp, ratio
+
+    def ratios(other):
+        out = {}
+        for key in ("store_GiBs", "fetch_GiBs"):
+            a, b = er.get(key), other.get(key)
+            if isinstance(a, dict) and isinstance(b, dict) and a["n"] == b["n"]:
+                per = [x / y for x, y in zip(a["samples"], b["samples"]) if y > 0]
+                if len(per) == a["n"]:
+                    out[key.replace("_GiBs", "")] = spread(per)
+        return out
+    return er, rp, ru, ratios(rp), ratios(ru)
 
 
 def plugin_lines(binary=PLUGIN_BIN, sizes=PLUGIN_SIZES, timeout=240, reps=PLUGIN_REPS):
@@ -952,9 +957,12 @@ def plugin_lines(binary=PLUGIN_BIN, sizes=PLUGIN_SIZES, timeout=240, reps=PLUGIN
                                stderr=subprocess.PIPE, timeout=timeout)
             line = r.stdout.decode(errors="replace").strip().splitlines()
             d = json.loads(line[-1]) if line else {}
-            er, rp, ratio = plugin_aggregate(d)
+            er, rp, ru, ratio, ratio_u = plugin_aggregate(d)
             row = {"ok": r.returncode == 0 and all(x in er for x in PLUGIN_KEYS),
                    "reps": d.get("reps"), "erasure": er, "replication": rp, "ratio": ratio}
+            if ru:
+                row["replication_unvalidated"] = ru
+                row["ratio_unvalidated"] = ratio_u
             if not row["ok"]:
                 row["note"] = "rc %d: %s" % (r.returncode, r.stderr.decode(errors="replace")[-300:])
         except (OSError, subprocess.SubprocessError, ValueError, IndexError) as ex:

@@ -525,7 +525,9 @@ def test_plugin_lines_parse_and_flag_failures(tmp_path):
                        "erasure": {k: [1.0, 3.0, 2.0, 5.0, 4.0] for k in bench.PLUGIN_KEYS} | {
                            "fetch_after_repair_ok": True, "unrecoverable": 0},
                        "replication": {"store_GiBs": [2.0, 2.0, 2.0, 2.0, 2.0],
-                                       "fetch_GiBs": [1.0, 1.0, 4.0, 1.0, 1.0]}})
+                                       "fetch_GiBs": [1.0, 1.0, 4.0, 1.0, 1.0]},
+                       "replication_unvalidated": {"store_GiBs": [4.0, 4.0, 4.0, 4.0, 4.0],
+                                                   "fetch_GiBs": [1.0, 1.0, 1.0, 1.0, 1.0]}})
     fake = tmp_path / "bench_plugin"
     fake.write_text("#!/bin/sh\n[ \"$1\" = 3 ] && { echo oops >&2; echo '%s'; exit 1; }\n"
                     "[ \"$1\" = 5 ] && { echo '{\"erasure\": {}}'; exit 0; }\n"
@@ -545,6 +547,10 @@ def test_plugin_lines_parse_and_flag_failures(tmp_path):
     assert row["ratio"]["store"]["median"] == 1.5
     assert row["ratio"]["fetch"]["samples"] == [1.0, 3.0, 0.5, 5.0, 4.0]
     assert row["ratio"]["fetch"]["median"] == 3.0 and row["ratio"]["fetch"]["min"] == 0.5
+    # the same against replication through plain peers
+    assert row["replication_unvalidated"]["store_GiBs"]["median"] == 4.0
+    assert row["ratio_unvalidated"]["store"]["samples"] == [0.25, 0.75, 0.5, 1.25, 1.0]
+    assert row["ratio_unvalidated"]["fetch"]["median"] == 3.0
     assert not out["3x4096"]["ok"] and "oops" in out["3x4096"]["note"]
     assert not out["5x64"]["ok"]
     gone = bench.plugin_lines(str(tmp_path / "missing"), [(1, 1)], timeout=30)
