@@ -547,7 +547,7 @@ void ShardLocal::validate(const Key& k, const uint8_t* v, size_t n) const {
   // (a repair rewriting a damaged copy), never another kind of value
   bool other = false;
   auto prev = [&](const uint8_t* p, size_t pn) { other = pn < 4 || std::memcmp(p, "MECS", 4) != 0; };
-  if (storage().read(k, prev) && other) throw ValidationFailed("shard: key holds another kind of value");
+  if (storage().read_prefix(k, 4, prev) && other) throw ValidationFailed("shard: key holds another kind of value");
 }
 
 std::unique_ptr<Local> make_shard_local(std::unique_ptr<Silo> storage) {

@@ -265,6 +265,13 @@ bool Silo::_read(const Key& k, const ReadSink& sink) const {
   return true;
 }
 
+bool Silo::_read_prefix(const Key& k, size_t n, const ReadSink& sink) const {
+  Buffer v;
+  if (!_try_get_prefix(k, n, v)) return false;
+  sink(v.data(), v.size());
+  return true;
+}
+
 bool Silo::_try_get(const Key& k, Buffer& out) const {
   try {
     out = _get(k);
@@ -316,6 +323,13 @@ bool MemorySilo::_read(const Key& k, const ReadSink& sink) const {
   const Value v = find(k);  // the reference keeps the bytes alive outside the lock
   if (!v.p) return false;
   sink(v.p.get(), v.n);
+  return true;
+}
+
+bool MemorySilo::_read_prefix(const Key& k, size_t n, const ReadSink& sink) const {
+  const Value v = find(k);
+  if (!v.p) return false;
+  sink(v.p.get(), std::min(n, v.n));
   return true;
 }
 
@@ -774,23 +788,24 @@ class ReplicaLocal : public Local {
   using Local::Local;
   void validate(const Key& k, const uint8_t* v, size_t n) const override {
     validate_replica(k, v, n);
-    // validate with the previous version, if any
-    bool stored_mutable = false;
-    uint32_t stored_version = 0;
-    std::unique_ptr<Block> current;
+    // validate with the previous version, if any: its version field (the
+    // first 4 bytes) for a mutable block, and the whole stored block only
+    // when it conflicts
     const uint32_t version = view_replica(v, n).version;
-    auto prev = [&](const uint8_t* p, size_t pn) {
-      const ReplicaView pv = view_replica(p, pn);
-      stored_mutable = k.mutable_block();
-      stored_version = pv.version;
-      if (stored_mutable && pv.version >= version)
-        current = std::make_unique<Block>(decode_replica(k, p, pn));
+    bool stored_newer = false;
+    uint32_t stored_version = 0;
+    auto head = [&](const uint8_t* p, size_t pn) {
+      if (pn < 4) throw ValidationFailed("stored value is no replica");
+      std::memcpy(&stored_version, p, 4);
+      stored_newer = stored_version >= version;
     };
-    if (!storage().read(k, prev)) return;
-    if (current)
-      throw Conflict("stored version " + std::to_string(stored_version) + " is not older than " +
-                         std::to_string(version),
-                     std::move(current));
+    if (!storage().read_prefix(k, 4, head) || !k.mutable_block() || !stored_newer) return;
+    std::unique_ptr<Block> current;
+    auto whole = [&](const uint8_t* p, size_t pn) { current = std::make_unique<Block>(decode_replica(k, p, pn)); };
+    if (!storage().read(k, whole)) return;  // erased meanwhile
+    throw Conflict("stored version " + std::to_string(stored_version) + " is not older than " +
+                       std::to_string(version),
+                   std::move(current));
   }
 };
 }  // namespace

@@ -265,6 +265,9 @@ class Silo {
   // instead of copied out; false when absent.  The fetch paths validate a
   // shard and copy its payload into place in one pass.
   bool read(const Key& k, const ReadSink& sink) const { return _read(k, sink); }
+  // read() of the value's first n bytes (all of it if shorter): a peer's
+  // check of the value a store replaces reads no more than it looks at.
+  bool read_prefix(const Key& k, size_t n, const ReadSink& sink) const { return _read_prefix(k, n, sink); }
   // insert: accept a new key; update: accept an existing key.
   int set(const Key& k, const Buffer& v, bool insert = true, bool update = false);
   // set() of a value the caller gives up (a silo may keep it without a copy)
@@ -286,6 +289,7 @@ class Silo {
   virtual bool _contains(const Key& k) const;                // default: _try_get
   virtual bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const;  // default: _try_get
   virtual bool _read(const Key& k, const ReadSink& sink) const;              // default: _try_get
+  virtual bool _read_prefix(const Key& k, size_t n, const ReadSink& sink) const;  // default: _try_get_prefix
   virtual int _set(const Key& k, const Buffer& v, bool insert, bool update) = 0;
   virtual int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) { return _set(k, v, insert, update); }
   // default: a copy through _set_moved
@@ -310,6 +314,7 @@ class MemorySilo : public Silo {
   bool _contains(const Key& k) const override;
   bool _try_get_prefix(const Key& k, size_t n, Buffer& out) const override;
   bool _read(const Key& k, const ReadSink& sink) const override;
+  bool _read_prefix(const Key& k, size_t n, const ReadSink& sink) const override;
   int _set(const Key& k, const Buffer& v, bool insert, bool update) override;
   int _set_moved(const Key& k, Buffer&& v, bool insert, bool update) override;
   int _set_shared(const Key& k, std::shared_ptr<const uint8_t> bytes, size_t n, bool insert,

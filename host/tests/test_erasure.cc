@@ -166,6 +166,47 @@ TEST(silo_memory_contract, false) {
   CHECK(s.list().empty());
 }
 
+// Values that share one allocation (Silo::set_shared, the store's framed
+// runs), views (Silo::read / read_prefix) and usage: each key holds exactly
+// its own bytes, usage counts each value's length, and replacing or erasing
+// one value leaves the others intact; a silo without sharing (filesystem)
+// keeps a copy.
+TEST(silo_shared_values_and_views, false) {
+  auto run = std::shared_ptr<uint8_t>(new uint8_t[300], std::default_delete<uint8_t[]>());
+  for (int i = 0; i < 300; ++i) run.get()[i] = (uint8_t)i;
+  Key ks[3] = {Address::random(flags::immutable_block), Address::random(flags::immutable_block),
+               Address::random(flags::immutable_block)};
+  MemorySilo s;
+  for (int i = 0; i < 3; ++i) s.set_shared(ks[i], std::shared_ptr<const uint8_t>(run, run.get() + 100 * i), 90);
+  CHECK(s.usage() == 270);
+  run.reset();  // the silo's values keep the allocation alive
+  for (int i = 0; i < 3; ++i) {
+    const Buffer v = s.get(ks[i]);
+    CHECK(v.size() == 90 && v[0] == (uint8_t)(100 * i) && v[89] == (uint8_t)(100 * i + 89));
+  }
+  size_t seen = 0;
+  uint8_t first = 0;
+  auto view = [&](const uint8_t* p, size_t n) {
+    seen = n;
+    first = p[0];
+  };
+  CHECK(s.read(ks[1], view) && seen == 90 && first == 100);
+  CHECK(s.read_prefix(ks[2], 4, view) && seen == 4 && first == 200);
+  CHECK(s.read_prefix(ks[2], 1000, view) && seen == 90);
+  CHECK(!s.read(Address::random(flags::immutable_block), view));
+  s.set(ks[1], bytes("replaced"), false, true);
+  CHECK(s.usage() == 188 && s.get(ks[1]) == bytes("replaced"));
+  CHECK(s.get(ks[0])[5] == 5 && s.get(ks[2])[5] == 205);
+  for (auto& k : ks) s.erase(k);
+  CHECK(s.usage() == 0 && s.list().empty());
+  // capacity counts shared values too
+  MemorySilo small(100);
+  auto r2 = std::shared_ptr<uint8_t>(new uint8_t[200](), std::default_delete<uint8_t[]>());
+  small.set_shared(ks[0], r2, 80);
+  CHECK_THROW(small.set_shared(ks[1], std::shared_ptr<const uint8_t>(r2, r2.get() + 100), 80),
+              silo::InsufficientSpace);
+}
+
 std::string temp_dir(const char* tag) {
   char tmpl[256];
   std::snprintf(tmpl, sizeof tmpl, "/tmp/memo_ec_%s_XXXXXX", tag);
@@ -202,6 +243,20 @@ TEST(silo_filesystem_contract, false) {
     s.erase(k1);
     CHECK_THROW(s.get(k1), silo::MissingKey);
     CHECK(s.usage() == 1000);
+    // shared values are copied to their files; views and prefix views read them
+    auto run = std::shared_ptr<uint8_t>(new uint8_t[64], std::default_delete<uint8_t[]>());
+    for (int i = 0; i < 64; ++i) run.get()[i] = (uint8_t)(i + 1);
+    s.set_shared(k1, std::shared_ptr<const uint8_t>(run, run.get() + 32), 32);
+    run.reset();
+    CHECK(s.get(k1).size() == 32 && s.get(k1)[0] == 33 && s.usage() == 1032);
+    size_t seen = 0;
+    uint8_t first = 0;
+    auto view = [&](const uint8_t* p, size_t n) {
+      seen = n;
+      first = p[0];
+    };
+    CHECK(s.read(k2, view) && seen == 1000 && first == 7);
+    CHECK(s.read_prefix(k1, 4, view) && seen == 4 && first == 33);
   }
   std::filesystem::remove_all(root);
 }
