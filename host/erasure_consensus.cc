@@ -1874,8 +1874,9 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
   struct Todo {
     Address a;
     Placement pl;
-    std::vector<int> lost;                       // shards to rebuild
-    std::vector<std::pair<int, Buffer>> surv;    // k validated survivor shards (wire)
+    std::vector<int> lost;      // shards to rebuild
+    std::vector<uint8_t> sidx;  // the k validated survivors' indices
+    Buffer surv;                // their payloads, k x Sb, read in place from the silos
     bool skip = false;
   };
   // Chunks of blocks whose survivors are held in memory at once: up to
@@ -1916,7 +1917,9 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         x.pl = it->second;
       }
       const ShardHeader ref = header_of(x.a, x.pl, 0);
+      const size_t Sb = ref.shard_size;
       const ShardKeys keys(x.a);
+      x.surv.resize((size_t)k * Sb);
       for (int i = 0; i < total; ++i) {
         const Address& o = i < (int)x.pl.holder.size() ? x.pl.holder[i] : Address();
         auto nd = o ? overlay_.node(o) : nullptr;
@@ -1926,19 +1929,26 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         }
         if (!nd->up) continue;  // unreachable for now: neither lost nor usable
         const Key key = keys(i);
-        if ((int)x.surv.size() < k) {
-          Buffer w;
+        if ((int)x.sidx.size() < k) {
+          // validated on the silo's view, the payload copied into its
+          // survivor slot (no copy of the whole shard)
           bool ok = false;
-          try {
-            if (nd->try_fetch(key, w)) {
-              const ShardHeader h = decode_shard(w, nullptr);
-              ok = h.index == i && h.same_block(ref);
+          auto take = [&](const uint8_t* w, size_t n) {
+            try {
+              const uint8_t* pay = nullptr;
+              const ShardHeader h = decode_shard_view(w, n, &pay);
+              if (h.index != i || !h.same_block(ref)) return;
+              if (Sb) std::memcpy(x.surv.data() + x.sidx.size() * Sb, pay, Sb);
+              ok = true;
+            } catch (ValidationFailed&) {
             }
+          };
+          try {
+            nd->try_read(key, take);
           } catch (Unavailable&) {
             continue;
-          } catch (ValidationFailed&) {
           }
-          if (ok) x.surv.emplace_back(i, std::move(w));
+          if (ok) x.sidx.push_back((uint8_t)i);
           else x.lost.push_back(i);
         } else if (!nd->has(key)) {
           x.lost.push_back(i);
@@ -1949,7 +1959,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     std::vector<Todo*> work;
     for (auto& x : todo) {
       if (x.skip || x.lost.empty()) continue;
-      if ((int)x.surv.size() < k) {
+      if ((int)x.sidx.size() < k) {
         ++rep.unrecoverable;
         continue;
       }
@@ -1964,7 +1974,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     std::map<std::pair<int, std::vector<uint8_t>>, std::vector<Todo*>> by_pat;
     for (auto* x : work) {
       std::vector<uint8_t> pat;
-      for (int s = 0; s < k; ++s) pat.push_back((uint8_t)x->surv[s].first);
+      pat.assign(x->sidx.begin(), x->sidx.end());
       for (int i : x->lost) pat.push_back((uint8_t)i);
       by_pat[{size_bucket(memo_ec_shard_size(x->pl.B, k)), std::move(pat)}].push_back(x);
     }
@@ -2035,17 +2045,16 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       const size_t Sb = memo_ec_shard_size(x.pl.B, k);
       for (int s = 0; s < k; ++s) {
         uint8_t* slot = rb.surv + (bi * k + s) * S;
-        std::memcpy(slot, x.surv[s].second.data() + ShardHeader::kSize, Sb);
+        std::memcpy(slot, x.surv.data() + (size_t)s * Sb, Sb);
         std::memset(slot + Sb, 0, S - Sb);
-        rb.sidx[bi * k + s] = (uint8_t)x.surv[s].first;
+        rb.sidx[bi * k + s] = x.sidx[s];
       }
       for (int r = 0; r < e; ++r) rb.lidx[bi * e + r] = (uint8_t)x.lost[r];
     });
     tm.lap("copy_in");
     pool_.parallel_for(units.size(), [&](size_t t) {
       Todo& x = *rbs[units[t].first].grp->items[rbs[units[t].first].b0 + units[t].second];
-      x.surv.clear();
-      x.surv.shrink_to_fit();
+      Buffer().swap(x.surv);
     });
     tm.lap("free");
     if (!rbs.empty()) {
