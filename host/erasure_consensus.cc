@@ -2088,25 +2088,29 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
       const size_t bi = units[t].second, S = rb.S;
       const int e = rb.grp->e;
       Todo& x = *rb.grp->items[rb.b0 + bi];
-      std::set<Address> taken;
+      // the block's other holders (at most k + m: a flat list)
+      std::vector<Address> taken;
+      taken.reserve(total);
       for (int i = 0; i < total; ++i)
         if (x.pl.holder[i] && std::find(x.lost.begin(), x.lost.end(), i) == x.lost.end())
-          taken.insert(x.pl.holder[i]);
+          taken.push_back(x.pl.holder[i]);
       auto cand = overlay_.allocate(x.a, (int)overlay_.size());
       const ShardKeys keys(x.a);
+      const ShardHeader hdr = header_of(x.a, x.pl, 0);
       size_t ci = 0;
       for (int r = 0; r < e; ++r) {
         const int i = x.lost[r];
         const Address old = x.pl.holder[i];
-        const Buffer wire = encode_shard(header_of(x.a, x.pl, i), rb.out + (bi * e + r) * S);
+        // framed once; each candidate's silo may keep a reference to it
+        auto wire = std::make_shared<Buffer>(encode_shard(hdr, rb.out + (bi * e + r) * S, i));
         x.pl.holder[i] = Address();
         while (ci < cand.size()) {
           auto& nd = cand[ci++];
-          if (taken.count(nd->id)) continue;
+          if (std::find(taken.begin(), taken.end(), nd->id) != taken.end()) continue;
           try {
-            nd->store(keys(i), wire);
+            nd->store_shared(keys(i), std::shared_ptr<const uint8_t>(wire, wire->data()), wire->size());
             x.pl.holder[i] = nd->id;
-            taken.insert(nd->id);
+            taken.push_back(nd->id);
             ++placed[t];
             break;
           } catch (Error&) {  // unreachable or full: the next candidate
