@@ -1106,7 +1106,7 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
                                                                     ShardHeader* hdr,
                                                                     bool parallel,
                                                                     std::vector<Node*>* from,
-                                                                    Buffer* block) {
+                                                                    Buffer* block, bool index_locked) {
   const int k = o_.k, total = o_.k + o_.m;
   // the shard keys (one SHA-256 for the block), outside the parallel fetches
   std::array<Key, MEMO_EC_MAX_K + MEMO_EC_MAX_M> keys;
@@ -1189,7 +1189,10 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
 
   std::vector<std::shared_ptr<Node>> holder(total);
   {
-    std::shared_lock<std::shared_mutex> g(index_mu_);
+    // index_locked: the caller holds a reader lock across its whole parallel
+    // gather (one lock for thousands of blocks instead of one each)
+    std::shared_lock<std::shared_mutex> g(index_mu_, std::defer_lock);
+    if (!index_locked) g.lock();
     auto it = index_.find(a);
     if (it != index_.end()) {
       ref = header_of(a, it->second, 0);
@@ -1273,12 +1276,12 @@ std::vector<std::pair<int, Buffer>> ErasureConsensus::gather_shards(const Addres
   return out;
 }
 
-ErasureConsensus::Gathered ErasureConsensus::collect(const Address& a, bool parallel) {
+ErasureConsensus::Gathered ErasureConsensus::collect(const Address& a, bool parallel, bool index_locked) {
   Gathered g;
   const int k = o_.k;
   try {
     bool any_down = false;
-    g.shards = gather_shards(a, k, any_down, &g.h, parallel, nullptr, &g.block);
+    g.shards = gather_shards(a, k, any_down, &g.h, parallel, nullptr, &g.block, index_locked);
     if (g.shards.empty()) {
       if (any_down) throw TooFewPeers("erasure: no shard reachable for " + a.hex());
       throw MissingBlock("missing block " + a.hex());
@@ -1517,7 +1520,14 @@ void ErasureConsensus::_fetch(const std::vector<AddressVersion>& request, Receiv
   }
   PhaseTimer tm("fetch_many");
   std::vector<Gathered> g(n);
-  pool_.parallel_for(imm.size(), [&](size_t t) { g[imm[t]] = collect(addresses[imm[t]], false); });
+  {
+    // one reader lock on the index for the whole parallel gather: a lock per
+    // block is an atomic add on one shared line from every pool thread (the
+    // gather tasks take no index lock of their own, and none of them waits
+    // for a writer)
+    std::shared_lock<std::shared_mutex> il(index_mu_);
+    pool_.parallel_for(imm.size(), [&](size_t t) { g[imm[t]] = collect(addresses[imm[t]], false, true); });
+  }
   tm.lap("gather");
   // degraded blocks by (S bucket, erasure pattern); patterns shared by at
   // least uniform_min blocks (a node down) take the uniform rebuild, the
@@ -1904,11 +1914,11 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
     // with include_down), lacks it, or holds a copy that fails validation
     // or belongs to another block or geometry; the first k valid shards
     // found are the survivors.
+    std::shared_lock<std::shared_mutex> scan_lock(index_mu_);  // for the whole scan (see _fetch)
     pool_.parallel_for(cn, [&](size_t t) {
       Todo& x = todo[t];
       x.a = blocks[c0 + t];
       {
-        std::shared_lock<std::shared_mutex> g(index_mu_);
         auto it = index_.find(x.a);
         if (it == index_.end()) {
           x.skip = true;  // removed meanwhile
@@ -1955,6 +1965,7 @@ ErasureConsensus::RepairReport ErasureConsensus::repair_blocks(const std::vector
         }
       }
     });
+    scan_lock.unlock();  // placement below takes the index exclusively
     tm.lap("scan");
     std::vector<Todo*> work;
     for (auto& x : todo) {

@@ -443,7 +443,8 @@ class ErasureConsensus : public StackedConsensus {
     std::exception_ptr err;
     const uint8_t* payload(size_t s) const;  // shards[s]'s S payload bytes
   };
-  Gathered collect(const Address& a, bool parallel);
+  // index_locked: the caller holds a reader lock on index_mu_
+  Gathered collect(const Address& a, bool parallel, bool index_locked = false);
   // The block from g's data shards and, for g.lost[r], the S bytes at
   // rebuilt + r * stride; checks the CHB address.
   std::unique_ptr<Block> assemble(const Address& a, Gathered& g, const uint8_t* rebuilt,
@@ -468,7 +469,7 @@ class ErasureConsensus : public StackedConsensus {
   std::vector<std::pair<int, Buffer>> gather_shards(const Address& a, int want, bool& any_down,
                                                     ShardHeader* hdr, bool parallel = true,
                                                     std::vector<Node*>* from = nullptr,
-                                                    Buffer* block = nullptr);
+                                                    Buffer* block = nullptr, bool index_locked = false);
   // A block whose reassembly failed its address, from another k-subset of
   // its reachable shards; the disagreeing shards rewritten (AddressMismatch
   // when no subset within verify_subsets matches).

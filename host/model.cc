@@ -319,17 +319,25 @@ bool MemorySilo::_try_get_prefix(const Key& k, size_t n, Buffer& out) const {
   return true;
 }
 
+// The sink runs under the stripe's lock, which keeps the value alive: no
+// reference count is taken (values framed in one run share one, and every
+// reader's increment and decrement would meet on its line).  Sinks must not
+// call back into the silo.
 bool MemorySilo::_read(const Key& k, const ReadSink& sink) const {
-  const Value v = find(k);  // the reference keeps the bytes alive outside the lock
-  if (!v.p) return false;
-  sink(v.p.get(), v.n);
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  auto it = st.blocks.find(k);
+  if (it == st.blocks.end()) return false;
+  sink(it->second.p.get(), it->second.n);
   return true;
 }
 
 bool MemorySilo::_read_prefix(const Key& k, size_t n, const ReadSink& sink) const {
-  const Value v = find(k);
-  if (!v.p) return false;
-  sink(v.p.get(), std::min(n, v.n));
+  Stripe& st = stripe(k);
+  std::lock_guard<std::mutex> g(st.mu);
+  auto it = st.blocks.find(k);
+  if (it == st.blocks.end()) return false;
+  sink(it->second.p.get(), std::min(n, it->second.n));
   return true;
 }
 

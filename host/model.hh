@@ -263,7 +263,8 @@ class Silo {
   bool contains(const Key& k) const { return _contains(k); }
   // The value handed to sink(bytes, size) -- a view valid during the call --
   // instead of copied out; false when absent.  The fetch paths validate a
-  // shard and copy its payload into place in one pass.
+  // shard and copy its payload into place in one pass.  The sink must not
+  // call back into this silo (the memory silo runs it under a lock).
   bool read(const Key& k, const ReadSink& sink) const { return _read(k, sink); }
   // read() of the value's first n bytes (all of it if shorter): a peer's
   // check of the value a store replaces reads no more than it looks at.
