@@ -1747,39 +1747,37 @@ void ErasureConsensus::_remove(Address a, RemoveSignature rs) {
   std::mutex emu;
   std::string refused;
   std::vector<std::pair<Address, OwedRemove>> deferred;  // holders down now
+  // One removal request per node (Consensus::remove_many sends one per
+  // peer, Consensus.cc:176-236), naming the shard keys it may hold; the
+  // holder checks each shard against the owner its header records (a header
+  // that does not parse is no shard of any block: removed).
+  const auto check = [&](const Key&, const Buffer& head) {
+    Address shard_owner = owner;
+    try {
+      shard_owner = decode_shard_header(head.data(), head.size()).owner;
+    } catch (ValidationFailed&) {
+    }
+    return chb_validate_remove(a, shard_owner, rs, owners_);
+  };
   pool_.parallel_for(targets.size(), [&](size_t t) {
     Node* nd = targets[t].node;
     const int i0 = targets[t].index < 0 ? 0 : targets[t].index;
     const int i1 = targets[t].index < 0 ? total : targets[t].index + 1;
-    for (int i = i0; i < i1; ++i) {
-      const Key key = keys(i);
-      try {
-        Buffer head;
-        if (!nd->try_fetch_prefix(key, ShardHeader::kSize, head)) continue;  // not here
-        // the holder's own check, against the owner its shard records (a
-        // header that does not parse is no shard of any block: removed)
-        Address shard_owner = owner;
-        try {
-          shard_owner = decode_shard_header(head.data(), head.size()).owner;
-        } catch (ValidationFailed&) {
-        }
-        const std::string why = chb_validate_remove(a, shard_owner, rs, owners_);
-        if (!why.empty()) {
-          std::lock_guard<std::mutex> g(emu);
-          refused = why;
-          continue;
-        }
-        nd->remove(key);
-        ++removed;
-      } catch (Unavailable&) {
-        // the node is down: remove its shard(s) when it returns (or drop
-        // the debt when it is evicted), so the block does not come back with
-        // it.  For a block of unknown placement, every index it might hold.
+    std::vector<Key> ks;
+    for (int i = i0; i < i1; ++i) ks.push_back(keys(i));
+    try {
+      std::string why;
+      removed += nd->remove_values(ks, ShardHeader::kSize, check, &why);
+      if (!why.empty()) {
         std::lock_guard<std::mutex> g(emu);
-        deferred.push_back({nd->id, OwedRemove{a, targets[t].index < 0 ? -1 : i, rs}});
-        break;
-      } catch (silo::MissingKey&) {
+        refused = why;
       }
+    } catch (Unavailable&) {
+      // the node is down: remove its shard(s) when it returns (or drop
+      // the debt when it is evicted), so the block does not come back with
+      // it.  For a block of unknown placement, every index it might hold.
+      std::lock_guard<std::mutex> g(emu);
+      deferred.push_back({nd->id, OwedRemove{a, targets[t].index, rs}});
     }
   });
   // owed removals: a known block's down holders; for a block of unknown
@@ -1837,21 +1835,19 @@ void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
     try {
       if (held_elsewhere(r.block, node)) continue;  // stored again by another client
       const ShardKeys keys(r.block);
-      for (int i = r.index < 0 ? 0 : r.index; i < (r.index < 0 ? total : r.index + 1); ++i) {
-        Buffer head;
-        if (!nd->try_fetch_prefix(keys(i), ShardHeader::kSize, head)) continue;
+      std::vector<Key> ks;
+      for (int i = r.index < 0 ? 0 : r.index; i < (r.index < 0 ? total : r.index + 1); ++i) ks.push_back(keys(i));
+      // one request to the returned node; a shard is removed only while the
+      // removal's signature validates against the owner its header records
+      nd->remove_values(ks, ShardHeader::kSize, [&](const Key&, const Buffer& head) {
         Address shard_owner;
         try {
           shard_owner = decode_shard_header(head.data(), head.size()).owner;
         } catch (ValidationFailed&) {
           // no shard of any block under this key: removed
         }
-        if (!chb_validate_remove(r.block, shard_owner, r.rs, owners_).empty()) continue;
-        try {
-          nd->remove(keys(i));
-        } catch (silo::MissingKey&) {
-        }
-      }
+        return chb_validate_remove(r.block, shard_owner, r.rs, owners_);
+      });
     } catch (Unavailable&) {
       still.push_back(r);  // down again
     }

@@ -568,7 +568,30 @@ Buffer Node::fetch(const Key& k) const {
 
 void Node::remove(const Key& k) {
   if (!up || evicted) throw Unavailable("node down");
+  ++remove_requests;
   silo->erase(k);
+}
+
+int Node::remove_values(const std::vector<Key>& keys, size_t prefix, const RemoveCheck& check,
+                        std::string* refused) {
+  if (!up || evicted) throw Unavailable("node down");
+  ++remove_requests;
+  int n = 0;
+  for (auto& k : keys) {
+    Buffer head;
+    if (!silo->try_get_prefix(k, prefix, head)) continue;  // not here
+    std::string why = check(k, head);
+    if (!why.empty()) {
+      if (refused) *refused = std::move(why);
+      continue;
+    }
+    try {
+      silo->erase(k);
+      ++n;
+    } catch (silo::MissingKey&) {  // erased meanwhile
+    }
+  }
+  return n;
 }
 
 bool Node::try_fetch(const Key& k, Buffer& out) const {

@@ -457,6 +457,16 @@ struct Node {
   bool try_fetch_prefix(const Key& k, size_t n, Buffer& out) const;
   void remove(const Key& k);
   bool has(const Key& k) const;
+  // One removal request naming several keys (Peer::remove(address, rs),
+  // doughnut/Peer.hh, answered by Local::remove, Local.cc:260-278, which
+  // checks the signature against what it stores): on the node, each key
+  // present has its first `prefix` bytes handed to `check`, and is erased
+  // when check returns "" (otherwise the refusal is kept).  Returns the
+  // number erased; throws Unavailable, once, when the node is down.
+  using RemoveCheck = std::function<std::string(const Key& k, const Buffer& head)>;
+  int remove_values(const std::vector<Key>& keys, size_t prefix, const RemoveCheck& check,
+                    std::string* refused = nullptr);
+  Counter remove_requests;  // remove() and remove_values() requests served
 };
 
 // overlay::Overlay (src/memo/overlay/Overlay.hh:34-188): allocate(address, n)

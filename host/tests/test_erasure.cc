@@ -1222,8 +1222,12 @@ TEST(remove_unknown_block_reaches_every_holder, true) {
   ErasureOptions o = net.o;
   o.rescan = false;
   ErasureConsensus other(std::make_unique<ReplicationConsensus>(net.overlay, 3), net.overlay, o);
+  std::vector<int64_t> before;
+  for (auto& n : net.nodes) before.push_back(n->remove_requests.load());
   remove(other, b.address);
   CHECK(net.shards(b.address, 14) == 0);
+  // one removal request per node, naming every shard key (not k+m requests)
+  for (size_t i = 0; i < net.nodes.size(); ++i) CHECK(net.nodes[i]->remove_requests.load() - before[i] == 1);
 }
 
 // A removal owed to a holder that was down is void when the block was
