@@ -569,6 +569,34 @@ TEST(chb_remove_group_key_rules, false) {
 
 // The pinned arena keeps a few batch buffers for reuse, never one larger
 // than kKeepMaxBytes (a node-loss fetch must not leave GBs pinned).
+// Node::remove_values: one request (one Unavailable when down), keys absent
+// skipped, each present key's prefix checked on the node, refusals kept.
+TEST(node_remove_values_is_one_checked_request, false) {
+  Overlay ov;
+  auto n = ov.add_node(Address::random(0), std::make_unique<MemorySilo>());
+  std::vector<Key> ks;
+  for (int i = 0; i < 4; ++i) ks.push_back(Address::random(0));
+  n->store(ks[0], bytes("allow-0 payload"));
+  n->store(ks[1], bytes("refuse-1"));
+  n->store(ks[3], bytes("allow-3"));
+  std::vector<std::string> seen;
+  auto check = [&](const Key&, const Buffer& head) {
+    const std::string h(head.begin(), head.end());
+    seen.push_back(h);
+    return h.rfind("allow", 0) == 0 ? std::string() : std::string("no authority");
+  };
+  std::string refused;
+  CHECK(n->remove_values(ks, 5, check, &refused) == 2);
+  CHECK(n->remove_requests.load() == 1);
+  CHECK(refused == "no authority");
+  CHECK(seen.size() == 3);  // ks[2] was never there
+  for (auto& h : seen) CHECK(h.size() == 5);  // the prefix only
+  CHECK(!n->has(ks[0]) && n->has(ks[1]) && !n->has(ks[3]));
+  ov.set_up(n->id, false);
+  CHECK_THROW(n->remove_values(ks, 5, check), Unavailable);
+  CHECK(n->remove_requests.load() == 1);  // refused before it was served
+}
+
 TEST(pinned_arena_drops_outsized_buffers, false) {
   PinnedArena a;
   {
