@@ -1862,10 +1862,15 @@ void ErasureConsensus::settle_removes(const Address& node, bool evicted) {
 bool ErasureConsensus::held_elsewhere(const Address& a, const Address& except) const {
   const int total = o_.k + o_.m;
   const ShardKeys keys(a);
+  std::vector<Key> ks;
+  for (int i = 0; i < total; ++i) ks.push_back(keys(i));
+  // one request per node, naming every shard key of the block
   for (auto& nd : overlay_.lookup(a, (int)overlay_.size())) {
-    if (nd->id == except || !nd->up) continue;
-    for (int i = 0; i < total; ++i)
-      if (nd->has(keys(i))) return true;
+    if (nd->id == except) continue;
+    try {
+      if (nd->holds_any(ks)) return true;
+    } catch (Unavailable&) {
+    }
   }
   return false;
 }

@@ -607,6 +607,13 @@ bool Node::try_fetch_prefix(const Key& k, size_t n, Buffer& out) const {
 
 bool Node::has(const Key& k) const { return silo->contains(k); }
 
+bool Node::holds_any(const std::vector<Key>& keys) const {
+  if (!up || evicted) throw Unavailable("node down");
+  for (auto& k : keys)
+    if (silo->contains(k)) return true;
+  return false;
+}
+
 namespace {
 // A handle that does not own the node (the overlay does): copying it touches
 // no reference count.

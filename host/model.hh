@@ -467,6 +467,9 @@ struct Node {
   int remove_values(const std::vector<Key>& keys, size_t prefix, const RemoveCheck& check,
                     std::string* refused = nullptr);
   Counter remove_requests;  // remove() and remove_values() requests served
+  // One request: does the node hold any of these keys?  Throws Unavailable
+  // when the node is down.
+  bool holds_any(const std::vector<Key>& keys) const;
 };
 
 // overlay::Overlay (src/memo/overlay/Overlay.hh:34-188): allocate(address, n)

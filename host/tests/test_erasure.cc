@@ -592,7 +592,9 @@ TEST(node_remove_values_is_one_checked_request, false) {
   CHECK(seen.size() == 3);  // ks[2] was never there
   for (auto& h : seen) CHECK(h.size() == 5);  // the prefix only
   CHECK(!n->has(ks[0]) && n->has(ks[1]) && !n->has(ks[3]));
+  CHECK(n->holds_any(ks) && !n->holds_any({ks[0], ks[2], ks[3]}));
   ov.set_up(n->id, false);
+  CHECK_THROW(n->holds_any(ks), Unavailable);
   CHECK_THROW(n->remove_values(ks, 5, check), Unavailable);
   CHECK(n->remove_requests.load() == 1);  // refused before it was served
 }
